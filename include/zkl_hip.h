@@ -1,0 +1,156 @@
+/*
+ * zkl_hip.h — C ABI of the MI355X-native zk-lisp segment prover (libzkl_hip.so).
+ *
+ * One call proves one zk-lisp execution segment and returns the bytes of the
+ * inner STARK proof, i.e. what the reference gets from
+ *   ZkWinterfellProver.prove(trace)           zk-lisp-proof-winterfell/src/prove.rs:225
+ * inside
+ *   prove_segment(...)                        zk-lisp-proof-winterfell/src/prove.rs:1057-1175
+ * (the call at prove.rs:1142, `prover.prove(trace)?`).  The Rust side would
+ * `Proof::from_bytes` the result and continue at prove.rs:1144.  The binding a
+ * maintainer adds on the Rust side is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - field elements are f128 (p = 2^128 - 45*2^40 + 1), canonical (< p),
+ *    little-endian limbs {lo, hi}; the same value `BaseElement::as_int()` gives.
+ *  - traces are column-major: element (col, row) at trace[col * n_rows + row].
+ *  - every function returns 0 on success and a negative ZKL_E_* code on failure;
+ *    zkl_hip_last_error() then returns a message (the reference maps failures to
+ *    prove::Error::Backend(String), prove.rs:225-227; same shape here).
+ *  - the library owns nothing the caller passed in; proof buffers it returns are
+ *    released with zkl_hip_free().
+ *  - one zkl_ctx per device; calls on one ctx are serialised internally, calls
+ *    on different ctx run concurrently (reference calls prove_segment from a
+ *    rayon pool, prove.rs:1020-1048).
+ */
+#ifndef ZKL_HIP_H
+#define ZKL_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZKL_ABI_VERSION 1
+
+enum {
+  ZKL_OK = 0,
+  ZKL_E_INVALID = -1,   /* bad argument / unsupported configuration */
+  ZKL_E_DEVICE = -2,    /* HIP runtime error */
+  ZKL_E_OOM = -3,       /* device or host allocation failed */
+  ZKL_E_INTERNAL = -4,  /* internal consistency check failed */
+};
+
+typedef struct { uint64_t lo, hi; } zkl_f128;
+
+/* winterfell::ProofOptions as built at prove.rs:963-972 + with_partitions(prove.rs:1121).
+ * field_extension: 1 = None (FieldExtension discriminant); only None is supported for
+ * step proofs.  batching_*: 0 = Linear (BatchingMethod discriminant). */
+typedef struct {
+  uint32_t num_queries;              /* CLI default 64 (zk-lisp-cli/src/main.rs:124-132) */
+  uint32_t blowup_factor;            /* 16 */
+  uint32_t grinding_factor;          /* 16 */
+  uint32_t field_extension;          /* 1 = None */
+  uint32_t fri_folding_factor;       /* 2 */
+  uint32_t fri_remainder_max_degree; /* 1 */
+  uint32_t batching_constraints;     /* 0 = Linear */
+  uint32_t batching_deep;            /* 0 = Linear */
+  uint32_t num_partitions;           /* select_partitions_for_trace, utils.rs:394-409 */
+  uint32_t hash_rate;                /* idem */
+} zkl_proof_options;
+
+#define ZKL_MAX_MAIN_SLOTS 8
+
+/* crate::AirPublicInputs (zk-lisp-proof-winterfell/src/lib.rs:75-95) flattened.
+ * `core` fields are the subset of zk_lisp_proof::pi::PublicInputs (pi.rs:62-88)
+ * that ZkLispAir::new / get_assertions / to_elements read.  main_args are given
+ * already flattened into base-field slots (utils::encode_main_args_to_slots). */
+typedef struct {
+  uint8_t program_id[32];
+  uint8_t program_commitment[32];
+  uint8_t merkle_root[32];
+  uint64_t feature_mask;          /* core.feature_mask (FM_* bits, pi.rs:23-28) */
+  uint64_t segment_feature_mask;  /* effective per-segment mask (prove.rs:1078-1083) */
+  uint32_t n_main_slots;
+  zkl_f128 main_slots[ZKL_MAX_MAIN_SLOTS];
+  uint32_t vm_out_reg;
+  uint32_t vm_out_row;
+  uint8_t vm_expected_bytes[32];
+  zkl_f128 rom_acc[3];
+  zkl_f128 pc_init;
+  zkl_f128 ram_gp_unsorted_in, ram_gp_unsorted_out, ram_gp_sorted_in, ram_gp_sorted_out;
+  zkl_f128 rom_s_in[3];
+  zkl_f128 rom_s_out[3];
+  uint32_t vm_usage_mask;
+  uint32_t ram_delta_clk_bits;
+} zkl_air_public_inputs;
+
+/* Per-stage wall times of the last proof on a ctx, milliseconds; stage names follow
+ * the reference's tracing events (prove.rs:464-513): trace_lde, trace_commit,
+ * coefficients, evaluator, constraint_commitment, ood, deep, fri, grind, queries. */
+#define ZKL_NUM_STAGES 10
+
+typedef struct zkl_ctx zkl_ctx;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+int zkl_hip_init(int device, zkl_ctx** out);
+void zkl_hip_destroy(zkl_ctx* ctx);
+const char* zkl_hip_last_error(const zkl_ctx* ctx); /* ctx may be NULL */
+void zkl_hip_free(uint8_t* buf);
+int zkl_hip_abi_version(void);
+
+/* ---- the drop-in: one segment proof ----------------------------------------
+ * Replaces ZkProver::prove -> winterfell::Prover::prove (prove.rs:174-257) for
+ * ZkLispAir + PoseidonHasher + MerkleTree + DefaultRandomCoin (prove.rs:425-437).
+ * trace: host pointer, column-major width x n_rows.  Output: Proof::to_bytes(). */
+int zkl_hip_prove_segment(zkl_ctx* ctx, const zkl_f128* trace, uint32_t width, uint32_t n_rows,
+                          const zkl_air_public_inputs* pi, const zkl_proof_options* opts,
+                          uint8_t** proof_out, size_t* proof_len);
+
+/* Same, with the trace already resident in HBM (device pointer on ctx's device,
+ * column-major).  Used by the multi-segment pipeline and by bench.py. */
+int zkl_hip_prove_segment_device(zkl_ctx* ctx, const void* d_trace, uint32_t width, uint32_t n_rows,
+                                 const zkl_air_public_inputs* pi, const zkl_proof_options* opts,
+                                 uint8_t** proof_out, size_t* proof_len);
+
+/* Stage timings (ms) of the last proof on ctx; returns number written. */
+int zkl_hip_stage_times(const zkl_ctx* ctx, double* out_ms, int max_n);
+
+/* Per-kernel-family device time (ms, HIP events) of the last proof; names are
+ * returned through *names as a static '\n'-separated list. */
+int zkl_hip_kernel_times(const zkl_ctx* ctx, double* out_ms, int max_n, const char** names);
+
+/* ---- reference helpers the host needs on its side ------------------------ */
+/* utils::select_partitions_for_trace (utils.rs:394-409). */
+void zkl_select_partitions(uint32_t trace_width, uint32_t trace_length,
+                           uint32_t* num_partitions, uint32_t* hash_rate);
+
+/* ---- stage entry points (parity tests call these through the same ABI) ----- */
+/* PoseidonHasher::hash_elements over each row of a column-major matrix, with the
+ * row partitioning Winterfell applies (partition_size, merge_many); d_* are device
+ * pointers on ctx's device.  digests_out: n_rows field elements (digest low 16 B). */
+int zkl_hip_hash_rows(zkl_ctx* ctx, const void* d_matrix, uint32_t n_cols, uint32_t n_rows,
+                      uint32_t num_partitions, uint32_t hash_rate, void* d_digests_out);
+/* MerkleTree::new over n_leaves digests (field-element form); writes all 2*n nodes
+ * (nodes[1] = root, nodes[n+i] = leaf i) to d_nodes_out. */
+int zkl_hip_merkle_tree(zkl_ctx* ctx, const void* d_leaves, uint32_t n_leaves, void* d_nodes_out);
+/* Coset low-degree extension of column-major n_cols x n_rows evaluations over
+ * GENERATOR * <w_{n*blowup}>; writes coefficients (n_cols x n_rows) and the LDE
+ * (n_cols x n_rows*blowup), both column-major, natural order. */
+int zkl_hip_lde(zkl_ctx* ctx, const void* d_values, uint32_t n_cols, uint32_t n_rows,
+                uint32_t blowup, void* d_coeffs_out, void* d_lde_out);
+
+/* ---- workload generator (host, not the measured path) -------------------- */
+/* Synthetic VM-only straight-line segment: 2^log_n rows, width 204
+ * ({vm, rom} layout), ops cycling Const/Add/Mov/Mul over r0..r7 with splitmix64
+ * immediates; trace built the way vm/trace/{mod,vm,rom}.rs build it.  Writes the
+ * column-major trace (204 x 2^log_n) and the AIR public inputs. */
+int zkl_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128* trace_out,
+                         zkl_air_public_inputs* pi_out, uint32_t* width_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,111 @@
+/*
+ * ORACLE — test infrastructure only.  CPU restatement of the reference algorithm for
+ * the zk-lisp segment-proof hot path (zk-lisp-proof-winterfell + winterfell 0.13.1).
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ *
+ * Parity status: pinned by BLAKE3 spec vectors and the published
+ * rollup-bench program commitment; the Poseidon/AIR/transcript layers follow the
+ * reference sources cited per function; the Winterfell 0.13.1 byte/transcript conventions
+ * (third-party, absent here) are a restatement from the published crate and are
+ * "parity unpinned" against real Winterfell output.
+ */
+#ifndef ORACLE_H
+#define ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include "f128.h"
+#include "../include/zkl_hip.h"
+
+/* ---------------- BLAKE3 ---------------- */
+void orc_blake3(const uint8_t *in, size_t len, uint8_t out32[32]);
+void orc_blake3_parts(const uint8_t *const *parts, const size_t *lens, int nparts, uint8_t out32[32]);
+
+/* ---------------- Poseidon (poseidon/mod.rs, poseidon/hasher.rs) ---------------- */
+#define POS_T 12
+#define POS_RATE 10
+#define POS_ROUNDS 27
+typedef struct {
+  fe dom[2];
+  fe mds[12][12];
+  fe rc[POS_ROUNDS][12];
+  int rounds;
+} pos_suite;
+
+void pos_suite_derive(const uint8_t suite_id[32], int rounds, pos_suite *out);
+const pos_suite *pos_hasher_suite(void); /* suite_id = [0;32], 27 rounds (hasher.rs:23) */
+void pos_permute(const pos_suite *s, fe st[12]);
+fe ro_from_slices(const char *domain, const uint8_t *const *parts, const size_t *lens, int nparts);
+fe fold_bytes32(const uint8_t b[32]);                     /* utils.rs:359-371 */
+fe be_from_le8(const uint8_t b32[32]);                      /* utils.rs:346-357 */
+fe sponge_bytes(const pos_suite *s, const char *domain, const uint8_t *data, size_t len); /* hasher.rs:144-231 */
+
+/* PoseidonHasher digests are 32 bytes: state[0] LE16 || 16 zero bytes; we carry the fe */
+fe ph_hash_bytes(const uint8_t *data, size_t len);          /* Hasher::hash       hasher.rs:62 */
+fe ph_merge(fe a, fe b);                                   /* Hasher::merge      hasher.rs:72 */
+fe ph_merge_many(const fe *d, size_t n);                   /* merge_many         hasher.rs:87 (n>0) */
+fe ph_merge_with_int(fe seed, uint64_t v);                 /* merge_with_int     hasher.rs:107 */
+fe ph_hash_elements(const fe *e, size_t n);                /* hash_elements      hasher.rs:126 */
+
+/* ROM t=3 constants (poseidon/mod.rs:186-261) */
+void rom_constants(const uint8_t suite_id[32], fe rc[POS_ROUNDS][3], fe mds[3][3]);
+/* commit::program_field_commitment (commit.rs:31-79) */
+void program_field_commitment(const uint8_t blake32[32], fe out[2]);
+
+/* ---------------- NTT helpers ---------------- */
+void ntt_inplace(fe *a, size_t n, int inverse);            /* natural order in/out */
+void coset_interpolate(fe *a, size_t n, fe offset);        /* evals over offset*<w_n> -> coeffs */
+void coset_evaluate(const fe *coeffs, size_t ncoef, fe *out, size_t n, fe offset);
+fe poly_eval(const fe *c, size_t n, fe x);
+
+/* ---------------- AIR (vm/air/ (all modules), vm/layout.rs) ---------------- */
+typedef struct {
+  int lanes_start, g_map, g_final, g_r_start, mask, r_start;
+  int op[17];         /* const, mov, add, sub, mul, neg, eq, select, sponge, assert, assert_bit,
+                         assert_range, divmod, div128, mulwide, load, store */
+  int sel_dst0, sel_a, sel_b, sel_c, sel_dst1, sel_s_bits, sel_s_active, imm, eq_inv;
+  int pi_prog, pc, rom_op_start, pose_active, gadget_b, rom_s;
+  int width;
+} zk_cols;
+void cols_for_config(int vm, int ram, int sponge, int merkle, int rom, zk_cols *c);
+
+#define MAX_TC 512
+typedef struct {
+  zk_cols cols;
+  int feat_poseidon, feat_vm, feat_vm_expect, feat_sponge, feat_merkle, feat_ram, rom_enabled;
+  uint32_t vm_usage_mask;
+  int commit_nonzero;
+  fe rom_rc[POS_ROUNDS][3], rom_mds[3][3];
+  fe rom_w0[59], rom_w1[59];
+  fe dom[2];
+  fe program_fe[2];
+  /* transition constraint degrees (base, has_cycle32) */
+  int n_tc;
+  int deg_base[MAX_TC];
+  /* assertions sorted (step, column) after dedup */
+  size_t n_assert;
+  uint32_t *as_col, *as_step;
+  fe *as_val;
+  size_t trace_len;
+  int ce_blowup, n_comp_cols;
+} zk_air;
+
+int air_new(zk_air *air, const zkl_air_public_inputs *pi, uint32_t width, size_t n);
+void air_free(zk_air *air);
+/* evaluate all transition constraints at a frame; periodic = 32 values */
+void air_eval_transition(const zk_air *air, const fe *cur, const fe *nxt, const fe *periodic, fe *out);
+void air_periodic_at(const zk_air *air, fe x, fe out[32]);
+
+/* ---------------- trace generator (vm/trace/ (vm, rom) subset) ---------------- */
+int orc_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128 *trace_out,
+                         zkl_air_public_inputs *pi_out, uint32_t *width_out);
+
+/* ---------------- prover / verifier ---------------- */
+int orc_prove_segment(const zkl_f128 *trace, uint32_t width, uint32_t n,
+                      const zkl_air_public_inputs *pi, const zkl_proof_options *opts,
+                      uint8_t **proof, size_t *len, int boundary_mode);
+int orc_verify_segment(const uint8_t *proof, size_t len, const zkl_air_public_inputs *pi,
+                       const zkl_proof_options *opts, char *err, size_t errlen);
+void orc_free(void *p);
+
+#endif

@@ -1,0 +1,223 @@
+/*
+ * ORACLE — test infrastructure only.
+ *
+ * Synthetic VM segment built the way the reference builds traces:
+ *   vm/trace/mod.rs:386-524     build_empty_trace / build_full_trace (schedule gates, pc, dom tags)
+ *   vm/trace/vm.rs:58-888       VmTraceBuilder::fill_table (Const/Mov/Add/Sub/Mul/Neg/End)
+ *   vm/trace/vm.rs:890-921      op_to_one_hot (ROM mirror)
+ *   vm/trace/rom.rs:29-108      RomTraceBuilder (t=3 accumulator)
+ *   vm/trace/mod.rs:80-235      SegmentLayout projection (we build the {vm,rom} layout directly)
+ *   prove.rs:292-423,1289-1392  AIR public inputs, vm_usage_mask
+ *   utils.rs:262-289            vm_output_from_trace
+ * Program: levels-1 ALU ops cycling Const/Add/Mov/Mul over r0..r7 (splitmix64 choices,
+ * immediates < 2^63) followed by End; program_id = BLAKE3 of a fixed descriptor string.
+ * The product has its own generator (zk-lisp_amd/csrc/tracegen.cpp); tests pin it to this one.
+ */
+#include <stdio.h>
+#include <string.h>
+#include "oracle.h"
+
+#define NR 8
+
+static uint64_t splitmix64(uint64_t *s) {
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+enum { OP_CONST = 0, OP_MOV = 1, OP_ADD = 2, OP_SUB = 3, OP_MUL = 4, OP_NEG = 5, OP_END = 99 };
+typedef struct { int kind; int dst, a, b; uint64_t imm; } synth_op;
+
+static void synth_program(uint64_t seed, size_t levels, synth_op *ops) {
+  uint64_t st = seed;
+  static const int cyc[4] = {OP_CONST, OP_ADD, OP_MOV, OP_MUL};
+  for (size_t l = 0; l + 1 < levels; l++) {
+    uint64_t r = splitmix64(&st);
+    ops[l].kind = cyc[l % 4];
+    ops[l].dst = (int)(r & 7);
+    ops[l].a = (int)((r >> 3) & 7);
+    ops[l].b = (int)((r >> 6) & 7);
+    ops[l].imm = ops[l].kind == OP_CONST ? (splitmix64(&st) >> 1) : 0;
+  }
+  ops[levels - 1].kind = OP_END;
+  ops[levels - 1].dst = ops[levels - 1].a = ops[levels - 1].b = 0;
+  ops[levels - 1].imm = 0;
+}
+
+static void set_fe(zkl_f128 *t, size_t n, int col, size_t row, fe v) {
+  t[(size_t)col * n + row].lo = (uint64_t)v;
+  t[(size_t)col * n + row].hi = (uint64_t)(v >> 64);
+}
+static fe get_fe(const zkl_f128 *t, size_t n, int col, size_t row) {
+  const zkl_f128 *e = &t[(size_t)col * n + row];
+  return ((fe)e->hi << 64) | e->lo;
+}
+static void set_sel(zkl_f128 *t, size_t n, size_t row, int start, int idx) {
+  for (int i = 0; i < NR; i++) set_fe(t, n, start + i, row, 0);
+  set_fe(t, n, start + idx, row, 1);
+}
+
+static fe rom_encode_row(const zk_cols *c, const zkl_f128 *t, size_t n, size_t row, const fe *w) {
+  fe sum = 0;
+  int k = 0;
+  for (int i = 0; i < 17; i++) sum = fe_add(sum, fe_mul(get_fe(t, n, c->op[i], row), w[k++]));
+  const int st[5] = {c->sel_dst0, c->sel_a, c->sel_b, c->sel_c, c->sel_dst1};
+  for (int s = 0; s < 5; s++)
+    for (int i = 0; i < NR; i++) sum = fe_add(sum, fe_mul(get_fe(t, n, st[s] + i, row), w[k++]));
+  return sum;
+}
+
+int orc_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128 *t, zkl_air_public_inputs *pi,
+                         uint32_t *width_out) {
+  if (log_n < 5 || log_n > 26) return -1;
+  size_t n = (size_t)1 << log_n, levels = n / 32;
+  zk_cols c;
+  cols_for_config(1, 0, 0, 0, 1, &c);
+  if (width_out) *width_out = (uint32_t)c.width;
+  if (!t) return 0;
+  memset(t, 0, (size_t)c.width * n * sizeof(zkl_f128));
+  memset(pi, 0, sizeof *pi);
+
+  char desc[128];
+  snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 seed=0x%016llx levels=%zu",
+           (unsigned long long)seed, levels);
+  uint8_t pid[32];
+  orc_blake3((const uint8_t *)desc, strlen(desc), pid);
+  pos_suite ps;
+  pos_suite_derive(pid, POS_ROUNDS, &ps);
+
+  synth_op *ops = (synth_op *)malloc(levels * sizeof(synth_op));
+  synth_program(seed, levels, ops);
+
+  /* build_empty_trace + pc + dom tags (mod.rs:386-470) */
+  for (size_t l = 0; l < levels; l++) {
+    size_t b = l * 32;
+    set_fe(t, n, c.g_map, b, 1);
+    set_fe(t, n, c.g_final, b + 28, 1);
+    for (int j = 0; j < POS_ROUNDS; j++) set_fe(t, n, c.g_r_start + j, b + 1 + j, 1);
+    for (size_t r = b; r < b + 32; r++) set_fe(t, n, c.pc, r, (fe)l);
+    set_fe(t, n, c.lanes_start + 10, b, ps.dom[0]);
+    set_fe(t, n, c.lanes_start + 11, b, ps.dom[1]);
+  }
+  /* VmTraceBuilder (vm.rs:58-888) */
+  fe regs[NR] = {0};
+  for (size_t l = 0; l < levels; l++) {
+    fe next[NR];
+    memcpy(next, regs, sizeof next);
+    size_t b = l * 32, rm = b, rf = b + 28;
+    if (l == 0) set_fe(t, n, c.pi_prog, 0, be_from_le8(pid));
+    const synth_op *op = &ops[l];
+    int onehot = -1;
+    switch (op->kind) {
+      case OP_CONST: onehot = 0; break;
+      case OP_MOV: onehot = 1; break;
+      case OP_ADD: onehot = 2; break;
+      case OP_SUB: onehot = 3; break;
+      case OP_MUL: onehot = 4; break;
+      case OP_NEG: onehot = 5; break;
+      default: break;
+    }
+    if (onehot >= 0) set_fe(t, n, c.rom_op_start + onehot, rm, 1);
+    for (int i = 0; i < NR; i++) set_fe(t, n, c.r_start + i, rm, regs[i]);
+    size_t rows[2] = {rm, rf};
+    for (int q = 0; q < 2 && onehot >= 0; q++) {
+      size_t row = rows[q];
+      set_fe(t, n, c.op[onehot], row, 1);
+      set_sel(t, n, row, c.sel_dst0, op->dst);
+      if (op->kind == OP_CONST) set_fe(t, n, c.imm, row, (fe)op->imm);
+      if (op->kind != OP_CONST) set_sel(t, n, row, c.sel_a, op->a);
+      if (op->kind == OP_ADD || op->kind == OP_SUB || op->kind == OP_MUL) set_sel(t, n, row, c.sel_b, op->b);
+    }
+    switch (op->kind) {
+      case OP_CONST: next[op->dst] = (fe)op->imm; break;
+      case OP_MOV: next[op->dst] = regs[op->a]; break;
+      case OP_ADD: next[op->dst] = fe_add(regs[op->a], regs[op->b]); break;
+      case OP_SUB: next[op->dst] = fe_sub(regs[op->a], regs[op->b]); break;
+      case OP_MUL: next[op->dst] = fe_mul(regs[op->a], regs[op->b]); break;
+      case OP_NEG: next[op->dst] = fe_neg(regs[op->a]); break;
+      default: break;
+    }
+    for (size_t r = rm + 1; r <= rf; r++)
+      for (int i = 0; i < NR; i++) set_fe(t, n, c.r_start + i, r, regs[i]);
+    for (size_t r = rf + 1; r < b + 32; r++)
+      for (int i = 0; i < NR; i++) set_fe(t, n, c.r_start + i, r, next[i]);
+    memcpy(regs, next, sizeof regs);
+  }
+  /* RomTraceBuilder (rom.rs:37-106) */
+  fe rc3[POS_ROUNDS][3], mds3[3][3], w0[59], w1[59];
+  rom_constants(pid, rc3, mds3);
+  {
+    fe a = fe_exp(3, 17), cur = fe_mul(a, 3);
+    for (int i = 0; i < 59; i++) { w0[i] = cur; cur = fe_mul(cur, 3); }
+    a = fe_exp(3, 1037); cur = fe_mul(a, 3);
+    for (int i = 0; i < 59; i++) { w1[i] = cur; cur = fe_mul(cur, 3); }
+  }
+  fe s0_prev = 0;
+  fe last_state[3] = {0, 0, 0};
+  for (size_t l = 0; l < levels; l++) {
+    size_t b = l * 32, rm = b, rf = b + 28;
+    fe s1 = rom_encode_row(&c, t, n, rm, w0), s2 = rom_encode_row(&c, t, n, rm, w1);
+    set_fe(t, n, c.rom_s, rm, s0_prev);
+    set_fe(t, n, c.rom_s + 1, rm, s1);
+    set_fe(t, n, c.rom_s + 2, rm, s2);
+    fe s[3] = {s0_prev, s1, s2};
+    for (int j = 0; j < POS_ROUNDS; j++) {
+      size_t r = b + 1 + j;
+      for (int i = 0; i < 3; i++) set_fe(t, n, c.rom_s + i, r, s[i]);
+      fe s3[3] = {fe_cube(s[0]), fe_cube(s[1]), fe_cube(s[2])};
+      fe y[3];
+      for (int i = 0; i < 3; i++)
+        y[i] = fe_add(fe_add(fe_add(fe_mul(mds3[i][0], s3[0]), fe_mul(mds3[i][1], s3[1])),
+                             fe_mul(mds3[i][2], s3[2])), rc3[j][i]);
+      for (int i = 0; i < 3; i++) set_fe(t, n, c.rom_s + i, r + 1, y[i]);
+      memcpy(s, y, sizeof s);
+    }
+    for (size_t r = rf + 1; r < b + 32; r++)
+      for (int i = 0; i < 3; i++) set_fe(t, n, c.rom_s + i, r, s[i]);
+    s0_prev = s[0];
+    memcpy(last_state, s, sizeof s);
+  }
+  free(ops);
+
+  /* AIR public inputs (prove.rs:292-423 with segment = whole trace) */
+  memcpy(pi->program_id, pid, 32);
+  memcpy(pi->program_commitment, pid, 32);
+  pi->feature_mask = 2;          /* FM_VM */
+  pi->segment_feature_mask = 2;
+  pi->n_main_slots = 0;
+  /* vm_output_from_trace_with_layout (utils.rs:262-289) */
+  pi->vm_out_reg = 0; pi->vm_out_row = 29;
+  for (size_t l = levels; l-- > 0;) {
+    size_t rf = l * 32 + 28;
+    int found = -1;
+    for (int i = 0; i < NR; i++) if (get_fe(t, n, c.sel_dst0 + i, rf) == 1) { found = i; break; }
+    if (found >= 0) { pi->vm_out_reg = (uint32_t)found; pi->vm_out_row = (uint32_t)(rf + 1); break; }
+  }
+  for (int i = 0; i < 3; i++) {
+    fe v = last_state[i];
+    pi->rom_acc[i].lo = (uint64_t)v; pi->rom_acc[i].hi = (uint64_t)(v >> 64);
+    fe in = get_fe(t, n, c.rom_s + i, 0);
+    pi->rom_s_in[i].lo = (uint64_t)in; pi->rom_s_in[i].hi = (uint64_t)(in >> 64);
+    fe out = get_fe(t, n, c.rom_s + i, (levels - 1) * 32 + 28);
+    pi->rom_s_out[i].lo = (uint64_t)out; pi->rom_s_out[i].hi = (uint64_t)(out >> 64);
+  }
+  fe pc0 = get_fe(t, n, c.pc, 0);
+  pi->pc_init.lo = (uint64_t)pc0; pi->pc_init.hi = (uint64_t)(pc0 >> 64);
+  /* compute_vm_usage_mask_for_trace (prove.rs:1289-1392): ALU-only program -> 0 */
+  uint32_t mask = 0;
+  for (size_t r = 0; r < n; r++) {
+    int at_final = (r % 32) == 28;
+    if (at_final && (get_fe(t, n, c.op[9], r) || get_fe(t, n, c.op[7], r))) mask |= 1u << 0;
+    if (at_final && get_fe(t, n, c.op[10], r)) mask |= 1u << 1;
+    if (at_final && get_fe(t, n, c.op[11], r)) mask |= 1u << 2;
+    if (at_final && get_fe(t, n, c.op[12], r)) mask |= 1u << 3;
+    if (at_final && get_fe(t, n, c.op[14], r)) mask |= 1u << 4;
+    if (at_final && get_fe(t, n, c.op[13], r)) mask |= 1u << 5;
+    if (at_final && get_fe(t, n, c.op[6], r)) mask |= 1u << 6;
+    if (get_fe(t, n, c.op[8], r)) mask |= 1u << 7;
+  }
+  pi->vm_usage_mask = mask;
+  pi->ram_delta_clk_bits = 0;
+  return 0;
+}
