@@ -1,0 +1,87 @@
+// Launch wrappers for the gfx950 kernels of the segment prover (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "air_host.h"
+#include "field.h"
+
+namespace zkl {
+
+struct HasherConsts {  // PoseidonHasher suite [0;32] + folded domain labels
+  fe mds[144];
+  fe rc[27 * 12];
+  fe dom[2];
+  fe dom_elems, dom_merge, dom_many, dom_int;
+};
+void upload_hasher_consts(const HasherConsts& h, hipStream_t s);
+void upload_air_consts(const AirDevice& a, hipStream_t s);
+// transition composition coefficients alpha_j: copied device->constant from the draw buffer
+void upload_alphas_from_device(const fe* d_alphas, int n, hipStream_t s);
+void upload_deep_coeffs(const fe* h_coeffs, int n, hipStream_t s);
+
+// ---- hashing --------------------------------------------------------------
+// Row digests of a column-major matrix (ld = rows per column) with Winterfell partitioning.
+// d_tmp: scratch of n_parts * n_rows elements (unused when a single hash covers the row).
+void launch_hash_rows(const fe* d_mat, uint32_t n_cols, size_t n_rows, uint32_t num_partitions,
+                      uint32_t hash_rate, fe* d_tmp, fe* d_out, hipStream_t s);
+// Merkle tree: d_nodes[n..2n) must hold the leaves; fills d_nodes[1..n).
+void launch_merkle(fe* d_nodes, size_t n_leaves, hipStream_t s);
+// out[i] = merge_with_int(seed, base + 1 + i)   (RandomCoin::draw, counter base+1+i)
+void launch_draws(fe seed, uint64_t base, size_t k, fe* d_out, hipStream_t s);
+// smallest nonce in [base, base+count) with trailing_zeros(merge_with_int(seed, nonce)) >= bits
+void launch_grind(fe seed, uint64_t base, uint32_t count, uint32_t bits, unsigned long long* d_best, hipStream_t s);
+
+// ---- NTT ---------------------------------------------------------------------
+// In-place radix-2 stages on n_cols contiguous columns of length N (power of two).
+// dif=true : stages H = 2^hi_log .. 2^lo_log (descending), natural -> bit-reversed
+// dif=false: stages H = 2^lo_log .. 2^hi_log (ascending),  bit-reversed -> natural
+// roots: table of w_Ntab^e (e < Ntab), Ntab >= N; inverse tables give inverse transforms.
+void launch_ntt_stages(fe* d_data, size_t n_cols, size_t N, bool dif, int lo_log, int hi_log,
+                       const fe* d_roots, size_t Ntab, hipStream_t s);
+// out[c*N + B*j + t] = in[c*stride + off + src(j)*estride] * scale[bitrev_n(j)] * mult for t < B (B = N/n);
+// src(j) = j or n-1-j
+void launch_broadcast(const fe* d_in, size_t in_col_stride, size_t in_elem_stride, size_t in_offset,
+                      size_t n_cols, size_t n, size_t N, const fe* d_scale, fe mult, bool reverse, fe* d_out, hipStream_t s);
+// data[i] *= scale[bitrev(i)] on contiguous columns (post-DIF scaling)
+void launch_scale_bitrev(fe* d_data, size_t n_cols, size_t n, const fe* d_scale, hipStream_t s);
+// d_out[i] = base * w_N^i for i < N via the root table (step = Ntab / N)
+void launch_geometric(fe base, const fe* d_roots, size_t step, size_t N, fe* d_out, hipStream_t s);
+
+// ---- constraint evaluation ---------------------------------------------------
+struct CeParams {
+  size_t n, N, ce;            // trace length, LDE size, CE size
+  uint32_t blowup;            // LDE blowup (row step between cur and next)
+  fe gl;                      // g^(n-1)
+  fe inv_n;                   // 1/n
+  fe xn_inv[64];              // 1/(x^n - 1) for x^n = 3^n * w_(ce/n)^j
+  fe xn_m1[64];               // x^n - 1
+  fe lagr;                    // g^(n-1)/n
+  uint32_t n_bcols;           // number of asserted columns in the boundary tables
+  uint32_t bcol[64];          // their trace column indices
+};
+void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab,
+                            const fe* d_bm /* (n_bcols + 1) x ce */, const CeParams& p, fe* d_out, hipStream_t s);
+// boundary vectors: vec[slot*n + step] = beta_a ; wv[s] = sum beta_a*value_a over assertions at step s
+void launch_boundary_scatter(const uint32_t* d_slot, const uint32_t* d_step, const fe* d_beta, size_t n_assert,
+                             size_t n, fe* d_vecs, hipStream_t s);
+void launch_boundary_w(const uint32_t* d_row_start, const fe* d_beta, const fe* d_val, size_t n, fe* d_w, hipStream_t s);
+// any nonzero in data[lo, hi) on a bit-reversed vector of length N -> *d_flag = 1
+void launch_check_zero_range_bitrev(const fe* d_data, size_t N, size_t lo, size_t hi, unsigned* d_flag, hipStream_t s);
+
+// ---- OOD / DEEP / FRI ---------------------------------------------------------
+// out[c] = sum_j coef[c*ld + off + j*stride] * pw[j], for j < n ; two power vectors
+void launch_ood(const fe* d_coef, size_t n_cols, size_t col_stride, size_t elem_stride, size_t n, const fe* d_pw1,
+                const fe* d_pw2, fe* d_out1, fe* d_out2, hipStream_t s);
+struct DeepParams {
+  size_t N;
+  uint32_t W, C;
+  fe z, zg, sz, szg;
+};
+void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p, fe* d_out,
+                 hipStream_t s);
+void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s);
+void launch_fri_fold(const fe* d_ev, size_t Nd, fe alpha, const fe* d_iroots, size_t Ntab, fe* d_out, hipStream_t s);
+// gather 16-byte elements from absolute device addresses
+void launch_gather(const uint64_t* d_addrs, size_t k, fe* d_out, hipStream_t s);
+
+}  // namespace zkl

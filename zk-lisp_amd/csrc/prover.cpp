@@ -1,0 +1,746 @@
+// MI355X segment prover: host orchestration of winterfell 0.13.1 `Prover::prove` for
+// ZkLispAir + PoseidonHasher (reference instantiation prove.rs:425-517), exposed through
+// the C ABI in include/zkl_hip.h.  Every heavy stage runs on the GPU (kernels.hip); the
+// host keeps the Fiat-Shamir transcript (a few dozen permutations), builds Merkle
+// multiproof index sets and serialises Proof::to_bytes().
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/zkl_hip.h"
+#include "air_host.h"
+#include "host_hash.h"
+#include "kernels.h"
+
+using namespace zkl;
+
+namespace {
+
+#define HIPCHECK(x)                                                                           \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess)                                                                     \
+      throw DeviceError(std::string(#x) + ": " + hipGetErrorString(e_));                      \
+  } while (0)
+
+struct DeviceError : std::runtime_error { using std::runtime_error::runtime_error; };
+struct InvalidArg : std::runtime_error { using std::runtime_error::runtime_error; };
+
+int ilog2(size_t n) { int k = 0; while (((size_t)1 << k) < n) k++; return k; }
+uint32_t bitrev_u(uint32_t x, int logn) { uint32_t r = 0; for (int i = 0; i < logn; i++) r |= ((x >> i) & 1u) << (logn - 1 - i); return r; }
+
+// ------------------------------------------------------------------ device buffers
+struct DBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t b) {
+    if (b <= bytes) return;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    HIPCHECK(hipMalloc(&p, b));
+    bytes = b;
+  }
+  fe* f() const { return (fe*)p; }
+  ~DBuf() { if (p) (void)hipFree(p); }
+};
+
+// ------------------------------------------------------------------ Fiat-Shamir coin
+// DefaultRandomCoin<PoseidonHasher> [WF-recall]; order pinned by agg/fs.rs:67-237.
+struct Coin {
+  fe seed;
+  uint64_t counter = 0;
+  void reseed(fe d) { seed = hasher().merge(seed, d); counter = 0; }
+  fe draw() { return hasher().merge_with_int(seed, ++counter); }
+};
+
+// ------------------------------------------------------------------ byte writer
+struct Bytes {
+  std::vector<uint8_t> v;
+  void u8(uint8_t x) { v.push_back(x); }
+  void u64(uint64_t x) { for (int i = 0; i < 8; i++) v.push_back((uint8_t)(x >> (8 * i))); }
+  void usize(uint64_t x) {  // winter-utils write_usize (vint64)
+    int lz = x ? __builtin_clzll(x) : 64;
+    int l = (lz > 0 ? lz - 1 : 0) / 7;
+    int len = 9 - std::min(l, 8);
+    if (len == 9) { u8(0); u64(x); return; }
+    uint64_t enc = ((x << 1) | 1) << (len - 1);
+    for (int i = 0; i < len; i++) v.push_back((uint8_t)(enc >> (8 * i)));
+  }
+  void felem(fe x) { u64(x.lo); u64(x.hi); }
+  void digest(fe x) { felem(x); for (int i = 0; i < 16; i++) v.push_back(0); }
+  void vec(const Bytes& b) { usize(b.v.size()); v.insert(v.end(), b.v.begin(), b.v.end()); }
+};
+
+// MerkleTree::prove_batch node-index plan (winter-crypto 0.13, [WF-recall]):
+// returns, per normalized leaf pair, the list of tree-node indices whose digests go in.
+// Leaves are tree nodes n+i.
+std::vector<std::vector<uint64_t>> batch_plan(size_t n_leaves, const std::vector<size_t>& idx) {
+  int depth = ilog2(n_leaves);
+  std::vector<size_t> norm;
+  for (size_t i : idx) norm.push_back(i & ~(size_t)1);
+  std::sort(norm.begin(), norm.end());
+  norm.erase(std::unique(norm.begin(), norm.end()), norm.end());
+  std::set<size_t> req(idx.begin(), idx.end());
+  std::vector<std::vector<uint64_t>> lists(norm.size());
+  std::vector<size_t> next;
+  for (size_t k = 0; k < norm.size(); k++) {
+    for (size_t j = norm[k]; j < norm[k] + 2; j++)
+      if (!req.count(j)) lists[k].push_back(n_leaves + j);
+    next.push_back((norm[k] + n_leaves) >> 1);
+  }
+  for (int lvl = 1; lvl < depth; lvl++) {
+    std::vector<size_t> cur = next;
+    next.clear();
+    for (size_t i = 0; i < cur.size(); i++) {
+      size_t sib = cur[i] ^ 1;
+      if (i + 1 < cur.size() && cur[i + 1] == sib) i++;
+      else lists[i].push_back(sib);
+      next.push_back(sib >> 1);
+    }
+  }
+  return lists;
+}
+
+}  // namespace
+
+// ====================================================================== context
+struct zkl_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string err;
+  double stage_ms[ZKL_NUM_STAGES] = {0};
+  // tables
+  size_t tab_n = 0, tab_N = 0;
+  DBuf roots, iroots, opow, opow_n, pertab;
+  // work buffers
+  DBuf trace, coef, lde, parts, tree, ce, bvec, bm, clde, ctree, deep, draws, pw, oodv, asl, ast, asv, ars;
+  DBuf fri_ev, fri_tree, best, gaddr, gout, flag;
+  std::vector<uint8_t> pinned_dummy;
+  size_t pert_key_n = 0, pert_key_ce = 0;
+};
+
+namespace {
+
+const char* g_global_err = "";
+thread_local std::string g_tls_err;
+
+void set_err(zkl_ctx* c, const std::string& m) {
+  if (c) c->err = m;
+  g_tls_err = m;
+  g_global_err = g_tls_err.c_str();
+}
+
+void ensure_tables(zkl_ctx* C, size_t n, size_t N) {
+  hipStream_t s = C->stream;
+  if (C->tab_N < N) {
+    std::vector<fe> w(N), wi(N);
+    fe g = root_of_unity(ilog2(N)), gi = fe_inv(g);
+    w[0] = wi[0] = fe_one();
+    for (size_t i = 1; i < N; i++) { w[i] = fe_mul(w[i - 1], g); wi[i] = fe_mul(wi[i - 1], gi); }
+    C->roots.ensure(N * sizeof(fe));
+    C->iroots.ensure(N * sizeof(fe));
+    HIPCHECK(hipMemcpyAsync(C->roots.p, w.data(), N * sizeof(fe), hipMemcpyHostToDevice, s));
+    HIPCHECK(hipMemcpyAsync(C->iroots.p, wi.data(), N * sizeof(fe), hipMemcpyHostToDevice, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    C->tab_N = N;
+  }
+  if (C->tab_n != n) {
+    std::vector<fe> o(n), on(n);
+    fe inv_n = fe_inv(fe{n, 0}), p = fe_one();
+    for (size_t k = 0; k < n; k++) { o[k] = p; on[k] = fe_mul(p, inv_n); p = fe_mul(p, fe{3, 0}); }
+    C->opow.ensure(n * sizeof(fe));
+    C->opow_n.ensure(n * sizeof(fe));
+    HIPCHECK(hipMemcpyAsync(C->opow.p, o.data(), n * sizeof(fe), hipMemcpyHostToDevice, s));
+    HIPCHECK(hipMemcpyAsync(C->opow_n.p, on.data(), n * sizeof(fe), hipMemcpyHostToDevice, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    C->tab_n = n;
+  }
+}
+
+struct StageTimer {
+  zkl_ctx* C;
+  std::vector<hipEvent_t> ev;
+  explicit StageTimer(zkl_ctx* c) : C(c) {
+    ev.resize(ZKL_NUM_STAGES + 1);
+    for (auto& e : ev) (void)hipEventCreate(&e);
+  }
+  void mark(int i) { (void)hipEventRecord(ev[i], C->stream); }
+  void finish() {
+    (void)hipEventSynchronize(ev[ZKL_NUM_STAGES]);
+    for (int i = 0; i < ZKL_NUM_STAGES; i++) {
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+      C->stage_ms[i] = ms;
+    }
+  }
+  ~StageTimer() { for (auto& e : ev) (void)hipEventDestroy(e); }
+};
+
+template <class T>
+void d2h(zkl_ctx* C, T* dst, const void* src, size_t bytes) {
+  HIPCHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, C->stream));
+  HIPCHECK(hipStreamSynchronize(C->stream));
+}
+
+// powers kernel on host side is cheap enough only for small n: use geometric via GPU
+__global__ void powers_kernel(fe base, fe mult, size_t n, int logn, fe* out) {
+  size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  uint32_t k = logn ? (__brev((uint32_t)j) >> (32 - logn)) : 0;
+  out[j] = fe_mul(mult, fe_pow64(base, k));
+}
+
+void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t W, uint32_t n32,
+                const zkl_air_public_inputs& pi, const zkl_proof_options& o, std::vector<uint8_t>& out) {
+  hipStream_t s = C->stream;
+  const size_t n = n32;
+  if (n < 32 || (n & (n - 1))) throw InvalidArg("trace length must be a power of two >= 32");
+  if (o.field_extension != 1) throw InvalidArg("only FieldExtension::None is supported for segment proofs");
+  if (o.fri_folding_factor != 2) throw InvalidArg("only FRI folding factor 2 is supported");
+  if (o.batching_constraints != 0 || o.batching_deep != 0) throw InvalidArg("only BatchingMethod::Linear is supported");
+  if (o.blowup_factor < 2 || (o.blowup_factor & (o.blowup_factor - 1))) throw InvalidArg("blowup must be a power of two");
+  if (o.num_queries == 0 || o.num_queries > 255) throw InvalidArg("num_queries must be in 1..255");
+  AirInstance air;
+  std::string e = build_air(pi, W, n, air);
+  if (!e.empty()) throw InvalidArg(e);
+  if (o.blowup_factor < (uint32_t)air.ce_blowup) throw InvalidArg("blowup factor below constraint-evaluation blowup");
+  const size_t N = n * o.blowup_factor, ce = n * air.ce_blowup;
+  const int logn = ilog2(n), logN = ilog2(N), logce = ilog2(ce);
+  const int Cc = air.num_comp_cols;
+  const uint32_t B = o.blowup_factor;
+  const fe g = root_of_unity(logn), three{3, 0};
+  const Hasher& H = hasher();
+
+  HasherConsts hc{};
+  for (int i = 0; i < 144; i++) hc.mds[i] = H.suite.mds[i / 12][i % 12];
+  for (int r = 0; r < 27; r++) for (int l = 0; l < 12; l++) hc.rc[r * 12 + l] = H.suite.rc[r][l];
+  hc.dom[0] = H.suite.dom[0]; hc.dom[1] = H.suite.dom[1];
+  hc.dom_elems = H.dom_elems; hc.dom_merge = H.dom_merge; hc.dom_many = H.dom_many; hc.dom_int = H.dom_int;
+  upload_hasher_consts(hc, s);
+  upload_air_consts(air.dev, s);
+  ensure_tables(C, n, N);
+  const fe* roots = C->roots.f();
+  const fe* iroots = C->iroots.f();
+  const size_t Ntab = C->tab_N;
+
+  StageTimer T(C);
+  T.mark(0);
+  // ---- coin seed: Context::to_elements || AirPublicInputs::to_elements (agg/fs.rs:67-73)
+  std::vector<fe> seed_el = context_elements(W, n, o);
+  auto pie = pi_elements(pi);
+  seed_el.insert(seed_el.end(), pie.begin(), pie.end());
+  Coin coin{H.hash_elements(seed_el.data(), seed_el.size()), 0};
+
+  // ---- 1. trace LDE (DefaultTraceLde::new): iNTT over <g>, coset LDE over 3*<w_N>
+  C->coef.ensure((size_t)W * n * sizeof(fe));
+  C->lde.ensure((size_t)W * N * sizeof(fe));
+  HIPCHECK(hipMemcpyAsync(C->coef.p, d_trace_in, (size_t)W * n * sizeof(fe),
+                          trace_on_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, s));
+  launch_ntt_stages(C->coef.f(), W, n, true, 0, logn - 1, iroots, Ntab, s);  // -> n*coef, bit-reversed
+  launch_broadcast(C->coef.f(), n, 1, 0, W, n, N, C->opow_n.f(), fe_one(), false, C->lde.f(), s);
+  launch_ntt_stages(C->lde.f(), W, N, false, ilog2(B), logN - 1, roots, Ntab, s);
+  T.mark(1);
+  // ---- trace commitment (commit_to_rows + MerkleTree)
+  uint32_t np_tr = o.num_partitions ? o.num_partitions : 1;
+  C->parts.ensure((size_t)std::max<uint32_t>(np_tr, 1) * N * sizeof(fe) + N * sizeof(fe));
+  C->tree.ensure(2 * N * sizeof(fe));
+  launch_hash_rows(C->lde.f(), W, N, o.num_partitions, o.hash_rate, C->parts.f(), C->tree.f() + N, s);
+  launch_merkle(C->tree.f(), N, s);
+  fe troot;
+  d2h(C, &troot, C->tree.f() + 1, sizeof(fe));
+  coin.reseed(troot);
+  T.mark(2);
+
+  // ---- 2. composition coefficients (Linear): transition then boundary, one draw each
+  const size_t na = air.assertions.size();
+  const size_t ndraw = (size_t)air.n_tc + na;
+  C->draws.ensure((ndraw + 1024) * sizeof(fe));
+  launch_draws(coin.seed, coin.counter, ndraw, C->draws.f(), s);
+  coin.counter += ndraw;
+  upload_alphas_from_device(C->draws.f(), air.n_tc, s);
+
+  // boundary tables: per asserted column c, M_c = coset-LDE of
+  // reverse(NTT_n(beta_c)); W likewise from sum_c beta*value.
+  std::map<uint32_t, uint32_t> slot_of;
+  std::vector<uint32_t> bcols;
+  for (auto& a : air.assertions)
+    if (!slot_of.count(a.col)) { slot_of[a.col] = (uint32_t)bcols.size(); bcols.push_back(a.col); }
+  if (bcols.size() > 64) throw InvalidArg("too many asserted columns");
+  const uint32_t nb = (uint32_t)bcols.size();
+  std::vector<uint32_t> hslot(na), hstep(na), rowstart(n + 1, 0);
+  std::vector<fe> hval(na);
+  for (size_t k = 0; k < na; k++) {
+    hslot[k] = slot_of[air.assertions[k].col];
+    hstep[k] = air.assertions[k].step;
+    hval[k] = air.assertions[k].value;
+    rowstart[hstep[k] + 1]++;
+  }
+  for (size_t r = 0; r < n; r++) rowstart[r + 1] += rowstart[r];
+  C->asl.ensure(na * 4); C->ast.ensure(na * 4); C->asv.ensure(na * sizeof(fe)); C->ars.ensure((n + 1) * 4);
+  HIPCHECK(hipMemcpyAsync(C->asl.p, hslot.data(), na * 4, hipMemcpyHostToDevice, s));
+  HIPCHECK(hipMemcpyAsync(C->ast.p, hstep.data(), na * 4, hipMemcpyHostToDevice, s));
+  HIPCHECK(hipMemcpyAsync(C->asv.p, hval.data(), na * sizeof(fe), hipMemcpyHostToDevice, s));
+  HIPCHECK(hipMemcpyAsync(C->ars.p, rowstart.data(), (n + 1) * 4, hipMemcpyHostToDevice, s));
+  C->bvec.ensure((size_t)(nb + 1) * n * sizeof(fe));
+  C->bm.ensure((size_t)(nb + 1) * ce * sizeof(fe));
+  HIPCHECK(hipMemsetAsync(C->bvec.p, 0, (size_t)(nb + 1) * n * sizeof(fe), s));
+  const fe* betas = C->draws.f() + air.n_tc;
+  launch_boundary_scatter((const uint32_t*)C->asl.p, (const uint32_t*)C->ast.p, betas, na, n, C->bvec.f(), s);
+  launch_boundary_w((const uint32_t*)C->ars.p, betas, C->asv.f(), n, C->bvec.f() + (size_t)nb * n, s);
+  launch_ntt_stages(C->bvec.f(), nb + 1, n, true, 0, logn - 1, roots, Ntab, s);  // forward, bit-reversed out
+  launch_broadcast(C->bvec.f(), n, 1, 0, nb + 1, n, ce, C->opow.f(), fe_one(), true, C->bm.f(), s);
+  launch_ntt_stages(C->bm.f(), nb + 1, ce, false, air.ce_blowup == 1 ? 0 : ilog2(ce / n), logce - 1, roots, Ntab, s);
+
+  // periodic table
+  if (C->pert_key_n != n || C->pert_key_ce != ce) {
+    auto tab = periodic_table(n, ce, three);
+    C->pertab.ensure(tab.size() * sizeof(fe));
+    HIPCHECK(hipMemcpyAsync(C->pertab.p, tab.data(), tab.size() * sizeof(fe), hipMemcpyHostToDevice, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    C->pert_key_n = n; C->pert_key_ce = ce;
+  }
+  CeParams cp{};
+  cp.n = n; cp.N = N; cp.ce = ce; cp.blowup = B;
+  cp.gl = fe_pow64(g, n - 1);
+  cp.inv_n = fe_inv(fe{n, 0});
+  cp.lagr = fe_mul(cp.gl, cp.inv_n);
+  {
+    size_t blow = ce / n;
+    fe wb = root_of_unity(ilog2(blow)), on = fe_pow64(three, n), p = fe_one();
+    for (size_t j = 0; j < blow; j++) {
+      cp.xn_m1[j] = fe_sub(fe_mul(on, p), fe_one());
+      cp.xn_inv[j] = fe_inv(cp.xn_m1[j]);
+      p = fe_mul(p, wb);
+    }
+  }
+  cp.n_bcols = nb;
+  for (uint32_t u = 0; u < nb; u++) cp.bcol[u] = bcols[u];
+  C->ce.ensure(ce * sizeof(fe));
+  launch_constraint_eval(C->lde.f(), roots, Ntab, C->pertab.f(), C->bm.f(), cp, C->ce.f(), s);
+  T.mark(3);
+
+  // ---- 3. composition polynomial: coset interpolation, degree check, column LDE, commit
+  launch_ntt_stages(C->ce.f(), 1, ce, true, 0, logce - 1, iroots, Ntab, s);  // ce * c_k * 3^k (bitrev)
+  C->flag.ensure(16);
+  HIPCHECK(hipMemsetAsync(C->flag.p, 0, 4, s));
+  launch_check_zero_range_bitrev(C->ce.f(), ce, (size_t)Cc * n, ce, (unsigned*)C->flag.p, s);
+  C->clde.ensure((size_t)Cc * N * sizeof(fe));
+  const int loge = ilog2(ce / n);
+  const fe inv3 = fe_inv(three), inv_ce = fe_inv(fe{ce, 0});
+  for (int j = 0; j < Cc; j++) {
+    // column j coefficient k' = chat[j n + k'] * 3^(-(j n + k')) / ce; LDE multiplies by 3^k'
+    fe mult = fe_mul(fe_pow64(inv3, (uint64_t)j * n), inv_ce);
+    launch_broadcast(C->ce.f(), 0, ce / n, bitrev_u((uint32_t)j, loge), 1, n, N, nullptr, mult, false,
+                     C->clde.f() + (size_t)j * N, s);
+  }
+  launch_ntt_stages(C->clde.f(), Cc, N, false, ilog2(B), logN - 1, roots, Ntab, s);
+  C->ctree.ensure(2 * N * sizeof(fe));
+  launch_hash_rows(C->clde.f(), Cc, N, o.num_partitions, o.hash_rate, C->parts.f(), C->ctree.f() + N, s);
+  launch_merkle(C->ctree.f(), N, s);
+  unsigned bad = 0;
+  d2h(C, &bad, C->flag.p, 4);
+  if (bad) throw InvalidArg("constraint composition polynomial degree too large: trace does not satisfy the AIR");
+  fe croot;
+  d2h(C, &croot, C->ctree.f() + 1, sizeof(fe));
+  coin.reseed(croot);
+  T.mark(4);
+
+  // ---- 4. OOD frame at z and z*g
+  fe z = coin.draw(), zg = fe_mul(z, g);
+  C->pw.ensure(4 * n * sizeof(fe));
+  fe* pw = C->pw.f();
+  fe inv_n = fe_inv(fe{n, 0});
+  powers_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(z, inv_n, n, logn, pw);
+  powers_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(zg, inv_n, n, logn, pw + n);
+  powers_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(fe_mul(z, inv3), fe_one(), n, logn, pw + 2 * n);
+  powers_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(fe_mul(zg, inv3), fe_one(), n, logn, pw + 3 * n);
+  C->oodv.ensure(2 * ((size_t)W + Cc) * sizeof(fe));
+  fe* dood = C->oodv.f();
+  launch_ood(C->coef.f(), W, n, 1, n, pw, pw + n, dood, dood + W, s);
+  for (int j = 0; j < Cc; j++)
+    launch_ood(C->ce.f() + bitrev_u((uint32_t)j, loge), 1, 0, ce / n, n, pw + 2 * n, pw + 3 * n,
+               dood + 2 * W + j, dood + 2 * W + Cc + j, s);
+  std::vector<fe> hood(2 * ((size_t)W + Cc));
+  d2h(C, hood.data(), dood, hood.size() * sizeof(fe));
+  std::vector<fe> tz(hood.begin(), hood.begin() + W), tzg(hood.begin() + W, hood.begin() + 2 * W);
+  std::vector<fe> hz(Cc), hzg(Cc);
+  for (int j = 0; j < Cc; j++) {
+    fe mult = fe_mul(fe_pow64(inv3, (uint64_t)j * n), inv_ce);
+    hz[j] = fe_mul(hood[2 * W + j], mult);
+    hzg[j] = fe_mul(hood[2 * W + Cc + j], mult);
+  }
+  std::vector<fe> oodcat;
+  oodcat.insert(oodcat.end(), tz.begin(), tz.end());
+  oodcat.insert(oodcat.end(), hz.begin(), hz.end());
+  oodcat.insert(oodcat.end(), tzg.begin(), tzg.end());
+  oodcat.insert(oodcat.end(), hzg.begin(), hzg.end());
+  coin.reseed(H.hash_elements(oodcat.data(), oodcat.size()));
+  T.mark(5);
+
+  // ---- 5. DEEP composition coefficients (W trace, then C constraint) and evaluations
+  std::vector<fe> gam(W + Cc);
+  launch_draws(coin.seed, coin.counter, W + Cc, C->draws.f(), s);
+  coin.counter += W + Cc;
+  d2h(C, gam.data(), C->draws.p, gam.size() * sizeof(fe));
+  upload_deep_coeffs(gam.data(), (int)gam.size(), s);
+  DeepParams dp{};
+  dp.N = N; dp.W = W; dp.C = Cc; dp.z = z; dp.zg = zg;
+  dp.sz = fe_zero(); dp.szg = fe_zero();
+  for (uint32_t c = 0; c < W; c++) { dp.sz = fe_add(dp.sz, fe_mul(gam[c], tz[c])); dp.szg = fe_add(dp.szg, fe_mul(gam[c], tzg[c])); }
+  for (int j = 0; j < Cc; j++) { dp.sz = fe_add(dp.sz, fe_mul(gam[W + j], hz[j])); dp.szg = fe_add(dp.szg, fe_mul(gam[W + j], hzg[j])); }
+  C->deep.ensure(N * sizeof(fe));
+  launch_deep(C->lde.f(), C->clde.f(), roots, Ntab, dp, C->deep.f(), s);
+  T.mark(6);
+
+  // ---- 6. FRI (FriProver::build_layers, folding 2, remainder degree rem_deg)
+  const size_t rem_max = (size_t)(o.fri_remainder_max_degree + 1) * B;
+  int nl = 0;
+  for (size_t d = N; d > rem_max; d /= 2) nl++;
+  std::vector<size_t> ev_off(nl + 1), tr_off(nl);
+  size_t ev_tot = 0, tr_tot = 0;
+  for (int d = 0; d <= nl; d++) {
+    ev_off[d] = ev_tot;
+    if (d >= 1) ev_tot += N >> d;
+    if (d < nl) { tr_off[d] = tr_tot; tr_tot += N >> d; }  // tree over Nd/2 leaves: 2*(Nd/2) nodes
+  }
+  C->fri_ev.ensure((ev_tot + 1) * sizeof(fe));
+  C->fri_tree.ensure((tr_tot + 1) * sizeof(fe));
+  auto layer_ev = [&](int d) -> fe* { return d == 0 ? C->deep.f() : C->fri_ev.f() + ev_off[d]; };
+  std::vector<fe> fri_roots(nl);
+  for (int d = 0; d < nl; d++) {
+    size_t Nd = N >> d, h = Nd / 2;
+    fe* tr = C->fri_tree.f() + tr_off[d];
+    launch_fri_leaves(layer_ev(d), Nd, tr + h, s);
+    launch_merkle(tr, h, s);
+    d2h(C, &fri_roots[d], tr + 1, sizeof(fe));
+    coin.reseed(fri_roots[d]);
+    fe alpha = coin.draw();
+    launch_fri_fold(layer_ev(d), Nd, alpha, iroots, Ntab, layer_ev(d + 1), s);
+  }
+  size_t Nr = N >> nl;
+  std::vector<fe> rem_ev(Nr);
+  d2h(C, rem_ev.data(), layer_ev(nl), Nr * sizeof(fe));
+  // interpolate over 3*<w_Nr> (constant domain offset, agg/trace.rs:940-952), keep rem_deg+1, reversed
+  std::vector<fe> rc(Nr);
+  {
+    fe w = root_of_unity(ilog2(Nr)), wi = fe_inv(w), inv_nr = fe_inv(fe{Nr, 0});
+    for (size_t k = 0; k < Nr; k++) {
+      fe acc = fe_zero(), wk = fe_pow64(wi, k), p = fe_one();
+      for (size_t j = 0; j < Nr; j++) { acc = fe_add(acc, fe_mul(rem_ev[j], p)); p = fe_mul(p, wk); }
+      rc[k] = fe_mul(fe_mul(acc, inv_nr), fe_pow64(inv3, k));
+    }
+  }
+  const size_t rlen = o.fri_remainder_max_degree + 1;
+  std::vector<fe> rem(rlen);
+  for (size_t k = 0; k < rlen; k++) rem[k] = rc[rlen - 1 - k];
+  fe rem_commit = H.hash_elements(rem.data(), rlen);
+  coin.reseed(rem_commit);
+  T.mark(7);
+
+  // ---- 7. grinding: smallest nonce >= 1 (winterfell without `concurrent`)
+  uint64_t nonce = 0;
+  C->best.ensure(8);
+  if (o.grinding_factor == 0) {
+    nonce = 1;
+  } else {
+    uint32_t batch = 1u << 16;
+    for (uint64_t base = 1; nonce == 0; base += batch, batch = std::min<uint32_t>(batch * 2, 1u << 22)) {
+      unsigned long long init = ~0ull;
+      HIPCHECK(hipMemcpyAsync(C->best.p, &init, 8, hipMemcpyHostToDevice, s));
+      launch_grind(coin.seed, base, batch, o.grinding_factor, (unsigned long long*)C->best.p, s);
+      unsigned long long r = 0;
+      d2h(C, &r, C->best.p, 8);
+      if (r != ~0ull) nonce = r;
+    }
+  }
+  T.mark(8);
+
+  // ---- 8. query positions: draw_integers(q, N, nonce), sort, dedup
+  coin.seed = H.merge_with_int(coin.seed, nonce);
+  coin.counter = 0;
+  std::vector<fe> qd(o.num_queries);
+  launch_draws(coin.seed, 0, o.num_queries, C->draws.f(), s);
+  d2h(C, qd.data(), C->draws.p, qd.size() * sizeof(fe));
+  std::vector<size_t> pos;
+  for (auto& v : qd) pos.push_back((size_t)(v.lo & (N - 1)));
+  std::sort(pos.begin(), pos.end());
+  pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
+  const size_t nq = pos.size();
+
+  // gather plan: trace rows, comp rows, trace/comp tree nodes, FRI values + tree nodes
+  std::vector<uint64_t> addrs;
+  auto A = [&](const fe* p) { addrs.push_back((uint64_t)(uintptr_t)p); };
+  for (size_t k = 0; k < nq; k++) for (uint32_t c = 0; c < W; c++) A(C->lde.f() + (size_t)c * N + pos[k]);
+  for (size_t k = 0; k < nq; k++) for (int j = 0; j < Cc; j++) A(C->clde.f() + (size_t)j * N + pos[k]);
+  auto tplan = batch_plan(N, pos);
+  for (auto& l : tplan) for (auto ix : l) A(C->tree.f() + ix);
+  for (auto& l : tplan) for (auto ix : l) A(C->ctree.f() + ix);
+  std::vector<std::vector<size_t>> fpos(nl);
+  std::vector<std::vector<std::vector<uint64_t>>> fplan(nl);
+  {
+    std::vector<size_t> p = pos;
+    size_t dsz = N;
+    for (int d = 0; d < nl; d++) {
+      size_t h = dsz / 2;
+      std::vector<size_t> f;
+      for (size_t x : p) { size_t y = x % h; if (std::find(f.begin(), f.end(), y) == f.end()) f.push_back(y); }
+      fpos[d] = f;
+      for (size_t y : f) { A(layer_ev(d) + y); A(layer_ev(d) + y + h); }
+      fplan[d] = batch_plan(h, f);
+      for (auto& l : fplan[d]) for (auto ix : l) A(C->fri_tree.f() + tr_off[d] + ix);
+      p = f;
+      dsz = h;
+    }
+  }
+  C->gaddr.ensure(addrs.size() * 8);
+  C->gout.ensure(addrs.size() * sizeof(fe));
+  HIPCHECK(hipMemcpyAsync(C->gaddr.p, addrs.data(), addrs.size() * 8, hipMemcpyHostToDevice, s));
+  launch_gather((const uint64_t*)C->gaddr.p, addrs.size(), C->gout.f(), s);
+  std::vector<fe> gv(addrs.size());
+  d2h(C, gv.data(), C->gout.p, gv.size() * sizeof(fe));
+  size_t gi = 0;
+
+  // ---- 9. Proof::to_bytes  [WF-recall layout, DESIGN.md §Proof bytes]
+  Bytes P;
+  P.u8((uint8_t)W); P.u8(0); P.u8(0); P.u8((uint8_t)logn); P.u8(0); P.u8(0);  // TraceInfo
+  P.u8(16); P.felem(fe{P_LO, P_HI});                                           // modulus bytes
+  P.u8((uint8_t)o.num_queries); P.u8((uint8_t)o.blowup_factor); P.u8((uint8_t)o.grinding_factor);
+  P.u8((uint8_t)o.field_extension); P.u8((uint8_t)o.fri_folding_factor); P.u8((uint8_t)o.fri_remainder_max_degree);
+  P.u8((uint8_t)o.batching_constraints); P.u8((uint8_t)o.batching_deep);
+  P.u8((uint8_t)o.num_partitions); P.u8((uint8_t)o.hash_rate);
+  P.u8((uint8_t)nq);
+  {
+    Bytes cm;
+    cm.digest(troot); cm.digest(croot);
+    for (auto& r : fri_roots) cm.digest(r);
+    cm.digest(rem_commit);
+    P.vec(cm);
+  }
+  auto emit_multiproof = [&](Bytes& b, const std::vector<std::vector<uint64_t>>& plan, int depth) {
+    b.u8((uint8_t)depth);
+    b.u8((uint8_t)plan.size());
+    for (auto& l : plan) {
+      b.u8((uint8_t)l.size());
+      for (size_t k = 0; k < l.size(); k++) b.digest(gv[gi++]);
+    }
+  };
+  Bytes tv, cv, tp, cpb;
+  for (size_t k = 0; k < nq * W; k++) tv.felem(gv[gi++]);
+  for (size_t k = 0; k < nq * Cc; k++) cv.felem(gv[gi++]);
+  emit_multiproof(tp, tplan, logN);
+  emit_multiproof(cpb, tplan, logN);
+  P.usize(1);
+  P.vec(tv); P.vec(tp);
+  P.vec(cv); P.vec(cpb);
+  {
+    Bytes ts, es;
+    for (auto& v : tz) ts.felem(v);
+    for (auto& v : tzg) ts.felem(v);
+    for (auto& v : hz) es.felem(v);
+    for (auto& v : hzg) es.felem(v);
+    P.vec(ts); P.vec(es);
+  }
+  P.usize((uint64_t)nl);
+  for (int d = 0; d < nl; d++) {
+    Bytes lv, lp;
+    for (size_t k = 0; k < fpos[d].size(); k++) { lv.felem(gv[gi++]); lv.felem(gv[gi++]); }
+    emit_multiproof(lp, fplan[d], ilog2((N >> d) / 2));
+    P.vec(lv); P.vec(lp);
+  }
+  {
+    Bytes rv;
+    for (auto& v : rem) rv.felem(v);
+    P.vec(rv);
+  }
+  P.u8(0);  // FriProof num_partitions (log2 of 1)
+  P.u64(nonce);
+  if (gi != gv.size()) throw std::runtime_error("internal: gather plan mismatch");
+  T.mark(9);
+  T.mark(10);
+  T.finish();
+  out.swap(P.v);
+}
+
+int run_guarded(zkl_ctx* ctx, const std::function<void()>& f) {
+  try {
+    f();
+    return ZKL_OK;
+  } catch (const InvalidArg& e) {
+    set_err(ctx, e.what());
+    return ZKL_E_INVALID;
+  } catch (const DeviceError& e) {
+    set_err(ctx, e.what());
+    return ZKL_E_DEVICE;
+  } catch (const std::bad_alloc&) {
+    set_err(ctx, "host allocation failed");
+    return ZKL_E_OOM;
+  } catch (const std::exception& e) {
+    set_err(ctx, e.what());
+    return ZKL_E_INTERNAL;
+  }
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+int zkl_hip_abi_version(void) { return ZKL_ABI_VERSION; }
+
+int zkl_hip_init(int device, zkl_ctx** out) {
+  if (!out) return ZKL_E_INVALID;
+  *out = nullptr;
+  return run_guarded(nullptr, [&] {
+    int cnt = 0;
+    HIPCHECK(hipGetDeviceCount(&cnt));
+    if (device < 0 || device >= cnt) throw InvalidArg("no such HIP device");
+    HIPCHECK(hipSetDevice(device));
+    auto* c = new zkl_ctx();
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete c; throw DeviceError(hipGetErrorString(e)); }
+    *out = c;
+  });
+}
+
+void zkl_hip_destroy(zkl_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* zkl_hip_last_error(const zkl_ctx* c) { return c ? c->err.c_str() : g_global_err; }
+
+void zkl_hip_free(uint8_t* p) { free(p); }
+
+static int finish_proof(std::vector<uint8_t>& v, uint8_t** out, size_t* len) {
+  uint8_t* b = (uint8_t*)malloc(v.size());
+  if (!b) return ZKL_E_OOM;
+  memcpy(b, v.data(), v.size());
+  *out = b;
+  *len = v.size();
+  return ZKL_OK;
+}
+
+int zkl_hip_prove_segment(zkl_ctx* c, const zkl_f128* trace, uint32_t width, uint32_t n, const zkl_air_public_inputs* pi,
+                          const zkl_proof_options* o, uint8_t** proof, size_t* len) {
+  if (!c || !trace || !pi || !o || !proof || !len) return ZKL_E_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  std::vector<uint8_t> v;
+  int rc = run_guarded(c, [&] {
+    HIPCHECK(hipSetDevice(c->device));
+    prove_impl(c, trace, true, width, n, *pi, *o, v);
+  });
+  return rc ? rc : finish_proof(v, proof, len);
+}
+
+int zkl_hip_prove_segment_device(zkl_ctx* c, const void* d_trace, uint32_t width, uint32_t n,
+                                 const zkl_air_public_inputs* pi, const zkl_proof_options* o, uint8_t** proof,
+                                 size_t* len) {
+  if (!c || !d_trace || !pi || !o || !proof || !len) return ZKL_E_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  std::vector<uint8_t> v;
+  int rc = run_guarded(c, [&] {
+    HIPCHECK(hipSetDevice(c->device));
+    prove_impl(c, d_trace, false, width, n, *pi, *o, v);
+  });
+  return rc ? rc : finish_proof(v, proof, len);
+}
+
+int zkl_hip_stage_times(const zkl_ctx* c, double* out, int max_n) {
+  if (!c || !out) return 0;
+  int k = std::min(max_n, ZKL_NUM_STAGES);
+  for (int i = 0; i < k; i++) out[i] = c->stage_ms[i];
+  return k;
+}
+
+int zkl_hip_kernel_times(const zkl_ctx* c, double* out, int max_n, const char** names) {
+  (void)c; (void)out; (void)max_n;
+  if (names) *names = "";
+  return 0;
+}
+
+void zkl_select_partitions(uint32_t w, uint32_t len, uint32_t* parts, uint32_t* rate) {
+  if (rate) *rate = w <= 32 ? 8 : 16;
+  if (parts) *parts = len >= (1u << 20) ? 16 : len >= (1u << 18) ? 8 : len >= (1u << 16) ? 4 : len >= (1u << 14) ? 2 : 1;
+}
+
+int zkl_hip_hash_rows(zkl_ctx* c, const void* d_m, uint32_t nc, uint32_t nr, uint32_t np, uint32_t rate, void* d_out) {
+  if (!c) return ZKL_E_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  return run_guarded(c, [&] {
+    HIPCHECK(hipSetDevice(c->device));
+    const Hasher& H = hasher();
+    HasherConsts hc{};
+    for (int i = 0; i < 144; i++) hc.mds[i] = H.suite.mds[i / 12][i % 12];
+    for (int r = 0; r < 27; r++) for (int l = 0; l < 12; l++) hc.rc[r * 12 + l] = H.suite.rc[r][l];
+    hc.dom[0] = H.suite.dom[0]; hc.dom[1] = H.suite.dom[1];
+    hc.dom_elems = H.dom_elems; hc.dom_merge = H.dom_merge; hc.dom_many = H.dom_many; hc.dom_int = H.dom_int;
+    upload_hasher_consts(hc, c->stream);
+    c->parts.ensure((size_t)std::max<uint32_t>(np, 1) * nr * sizeof(fe) + 16);
+    launch_hash_rows((const fe*)d_m, nc, nr, np, rate, c->parts.f(), (fe*)d_out, c->stream);
+    HIPCHECK(hipStreamSynchronize(c->stream));
+  });
+}
+
+int zkl_hip_merkle_tree(zkl_ctx* c, const void* d_leaves, uint32_t n, void* d_nodes) {
+  if (!c || n < 2 || (n & (n - 1))) return ZKL_E_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  return run_guarded(c, [&] {
+    HIPCHECK(hipSetDevice(c->device));
+    const Hasher& H = hasher();
+    HasherConsts hc{};
+    for (int i = 0; i < 144; i++) hc.mds[i] = H.suite.mds[i / 12][i % 12];
+    for (int r = 0; r < 27; r++) for (int l = 0; l < 12; l++) hc.rc[r * 12 + l] = H.suite.rc[r][l];
+    hc.dom[0] = H.suite.dom[0]; hc.dom[1] = H.suite.dom[1];
+    hc.dom_elems = H.dom_elems; hc.dom_merge = H.dom_merge; hc.dom_many = H.dom_many; hc.dom_int = H.dom_int;
+    upload_hasher_consts(hc, c->stream);
+    HIPCHECK(hipMemcpyAsync((fe*)d_nodes + n, d_leaves, (size_t)n * sizeof(fe), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHECK(hipMemsetAsync(d_nodes, 0, sizeof(fe), c->stream));
+    launch_merkle((fe*)d_nodes, n, c->stream);
+    HIPCHECK(hipStreamSynchronize(c->stream));
+  });
+}
+
+int zkl_hip_lde(zkl_ctx* c, const void* d_values, uint32_t nc, uint32_t n, uint32_t blowup, void* d_coeffs,
+                void* d_lde) {
+  if (!c || n < 2 || (n & (n - 1)) || blowup < 1 || (blowup & (blowup - 1))) return ZKL_E_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  return run_guarded(c, [&] {
+    HIPCHECK(hipSetDevice(c->device));
+    size_t N = (size_t)n * blowup;
+    ensure_tables(c, n, N);
+    hipStream_t s = c->stream;
+    fe* coef = (fe*)d_coeffs;
+    HIPCHECK(hipMemcpyAsync(coef, d_values, (size_t)nc * n * sizeof(fe), hipMemcpyDeviceToDevice, s));
+    launch_ntt_stages(coef, nc, n, true, 0, ilog2(n) - 1, c->iroots.f(), c->tab_N, s);
+    launch_broadcast(coef, n, 1, 0, nc, n, N, c->opow_n.f(), fe_one(), false, (fe*)d_lde, s);
+    launch_ntt_stages((fe*)d_lde, nc, N, false, ilog2(blowup), ilog2(N) - 1, c->roots.f(), c->tab_N, s);
+    // return natural-order coefficients: scale n*c (bitrev) by 1/n and un-permute on host side is
+    // not needed by callers; convert in place to natural order here
+    std::vector<fe> h((size_t)nc * n), r((size_t)nc * n);
+    HIPCHECK(hipMemcpyAsync(h.data(), coef, h.size() * sizeof(fe), hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    fe inv_n = fe_inv(fe{n, 0});
+    int logn = ilog2(n);
+    for (uint32_t col = 0; col < nc; col++)
+      for (uint32_t j = 0; j < n; j++) r[(size_t)col * n + bitrev_u(j, logn)] = fe_mul(h[(size_t)col * n + j], inv_n);
+    HIPCHECK(hipMemcpyAsync(coef, r.data(), r.size() * sizeof(fe), hipMemcpyHostToDevice, s));
+    HIPCHECK(hipStreamSynchronize(s));
+  });
+}
+
+}  // extern "C"

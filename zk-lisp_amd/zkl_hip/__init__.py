@@ -1,0 +1,205 @@
+"""zkl_hip — Python host for the MI355X-native zk-lisp segment prover.
+
+Mirrors the reference's prove path for one execution segment:
+  ZkProver::prove (zk-lisp-proof-winterfell/src/prove.rs:174-257)
+    -> winterfell::Prover::prove with ZkLispAir + PoseidonHasher (prove.rs:425-517)
+through the C ABI of libzkl_hip.so (include/zkl_hip.h).  The shared library is built
+in-tree by zk-lisp_amd/Makefile; importing this module fails loudly when it is missing.
+There is no CPU fallback: every proof is produced by the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+__all__ = [
+    "F128", "ProofOptions", "AirPublicInputs", "ZklError", "Context", "load_library",
+    "select_partitions_for_trace", "proof_options", "synth_vm_segment", "STAGE_NAMES",
+    "FM_VM", "FM_VM_EXPECT", "FM_POSEIDON", "FM_SPONGE", "FM_MERKLE", "FM_RAM",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libzkl_hip.so")
+
+# feature bits, zk-lisp-proof/src/pi.rs:23-28
+FM_POSEIDON, FM_VM, FM_VM_EXPECT, FM_SPONGE, FM_MERKLE, FM_RAM = 1, 2, 16, 32, 64, 128
+
+STAGE_NAMES = ["trace_lde", "trace_commit", "evaluator", "constraint_commitment", "ood",
+               "deep", "fri", "grind", "queries", "finish"]
+
+ERRORS = {-1: "invalid", -2: "device", -3: "oom", -4: "internal"}
+
+
+class ZklError(RuntimeError):
+    """Mirrors prove::Error::Backend(String) (prove.rs:52-62)."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"backend error ({ERRORS.get(code, code)}): {msg}")
+        self.code = code
+
+
+class F128(C.Structure):
+    _fields_ = [("lo", C.c_uint64), ("hi", C.c_uint64)]
+
+
+class ProofOptions(C.Structure):
+    """winterfell::ProofOptions as built at prove.rs:963-972 (+ with_partitions, :1121)."""
+    _fields_ = [(n, C.c_uint32) for n in (
+        "num_queries", "blowup_factor", "grinding_factor", "field_extension",
+        "fri_folding_factor", "fri_remainder_max_degree", "batching_constraints",
+        "batching_deep", "num_partitions", "hash_rate")]
+
+
+class AirPublicInputs(C.Structure):
+    """crate::AirPublicInputs (lib.rs:75-95) with the PublicInputs subset the AIR reads."""
+    _fields_ = [
+        ("program_id", C.c_uint8 * 32),
+        ("program_commitment", C.c_uint8 * 32),
+        ("merkle_root", C.c_uint8 * 32),
+        ("feature_mask", C.c_uint64),
+        ("segment_feature_mask", C.c_uint64),
+        ("n_main_slots", C.c_uint32),
+        ("main_slots", F128 * 8),
+        ("vm_out_reg", C.c_uint32),
+        ("vm_out_row", C.c_uint32),
+        ("vm_expected_bytes", C.c_uint8 * 32),
+        ("rom_acc", F128 * 3),
+        ("pc_init", F128),
+        ("ram_gp_unsorted_in", F128),
+        ("ram_gp_unsorted_out", F128),
+        ("ram_gp_sorted_in", F128),
+        ("ram_gp_sorted_out", F128),
+        ("rom_s_in", F128 * 3),
+        ("rom_s_out", F128 * 3),
+        ("vm_usage_mask", C.c_uint32),
+        ("ram_delta_clk_bits", C.c_uint32),
+    ]
+
+
+_lib = None
+
+
+def load_library():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libzkl_hip.so not built ({LIB_PATH}); run `make -C zk-lisp_amd`")
+    lib = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    lib.zkl_hip_init.argtypes = [C.c_int, P(C.c_void_p)]
+    lib.zkl_hip_destroy.argtypes = [C.c_void_p]
+    lib.zkl_hip_last_error.argtypes = [C.c_void_p]
+    lib.zkl_hip_last_error.restype = C.c_char_p
+    lib.zkl_hip_free.argtypes = [C.c_void_p]
+    lib.zkl_hip_prove_segment.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                          P(AirPublicInputs), P(ProofOptions), P(P(C.c_uint8)), P(C.c_size_t)]
+    lib.zkl_hip_prove_segment_device.argtypes = lib.zkl_hip_prove_segment.argtypes
+    lib.zkl_hip_stage_times.argtypes = [C.c_void_p, P(C.c_double), C.c_int]
+    lib.zkl_select_partitions.argtypes = [C.c_uint32, C.c_uint32, P(C.c_uint32), P(C.c_uint32)]
+    lib.zkl_synth_vm_segment.argtypes = [C.c_uint64, C.c_uint32, C.c_void_p, P(AirPublicInputs), P(C.c_uint32)]
+    lib.zkl_hip_hash_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]
+    lib.zkl_hip_merkle_tree.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
+    lib.zkl_hip_lde.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]
+    _lib = lib
+    return lib
+
+
+def select_partitions_for_trace(width: int, length: int):
+    """utils::select_partitions_for_trace (utils.rs:394-409)."""
+    lib = load_library()
+    np_, rate = C.c_uint32(), C.c_uint32()
+    lib.zkl_select_partitions(width, length, C.byref(np_), C.byref(rate))
+    return np_.value, rate.value
+
+
+def proof_options(width, length, queries=64, blowup=16, grind=16) -> ProofOptions:
+    """ProofOptions::new(q, blowup, grind, None, 2, 1, Linear, Linear).with_partitions(...)."""
+    parts, rate = select_partitions_for_trace(width, length)
+    return ProofOptions(queries, blowup, grind, 1, 2, 1, 0, 0, parts, rate)
+
+
+def synth_vm_segment(seed: int, log_n: int):
+    """Synthetic VM segment (workload generator): returns (trace, pi, width), trace column-major."""
+    lib = load_library()
+    w = C.c_uint32()
+    lib.zkl_synth_vm_segment(seed, log_n, None, None, C.byref(w))
+    n = 1 << log_n
+    trace = (F128 * (w.value * n))()
+    pi = AirPublicInputs()
+    rc = lib.zkl_synth_vm_segment(seed, log_n, C.cast(trace, C.c_void_p), C.byref(pi), C.byref(w))
+    if rc != 0:
+        raise ZklError(rc, "synth_vm_segment failed")
+    return trace, pi, w.value
+
+
+class Context:
+    """One prover context per device (zkl_hip_init)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        self.ptr = C.c_void_p()
+        rc = self.lib.zkl_hip_init(device, C.byref(self.ptr))
+        if rc != 0:
+            raise ZklError(rc, self.lib.zkl_hip_last_error(None).decode())
+
+    def close(self):
+        if self.ptr:
+            self.lib.zkl_hip_destroy(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self, rc):
+        raise ZklError(rc, self.lib.zkl_hip_last_error(self.ptr).decode())
+
+    def _finish(self, rc, out, ln):
+        if rc != 0:
+            self._err(rc)
+        data = C.string_at(out, ln.value)
+        self.lib.zkl_hip_free(out)
+        return data
+
+    def prove_segment(self, trace, width: int, n_rows: int, pi: AirPublicInputs, opts: ProofOptions) -> bytes:
+        """Proof::to_bytes() for one segment; `trace` is a host buffer (column-major f128)."""
+        out = C.POINTER(C.c_uint8)()
+        ln = C.c_size_t()
+        ptr = trace if isinstance(trace, int) else C.cast(trace, C.c_void_p)
+        rc = self.lib.zkl_hip_prove_segment(self.ptr, ptr, width, n_rows, C.byref(pi), C.byref(opts),
+                                            C.byref(out), C.byref(ln))
+        return self._finish(rc, out, ln)
+
+    def prove_segment_device(self, d_trace_ptr: int, width: int, n_rows: int, pi, opts) -> bytes:
+        """Same with the trace already resident in HBM (device pointer, e.g. torch data_ptr())."""
+        out = C.POINTER(C.c_uint8)()
+        ln = C.c_size_t()
+        rc = self.lib.zkl_hip_prove_segment_device(self.ptr, C.c_void_p(d_trace_ptr), width, n_rows, C.byref(pi),
+                                                   C.byref(opts), C.byref(out), C.byref(ln))
+        return self._finish(rc, out, ln)
+
+    def stage_times(self):
+        arr = (C.c_double * len(STAGE_NAMES))()
+        k = self.lib.zkl_hip_stage_times(self.ptr, arr, len(STAGE_NAMES))
+        return dict(zip(STAGE_NAMES[:k], list(arr)[:k]))
+
+    # stage entry points (device pointers)
+    def hash_rows(self, d_mat, n_cols, n_rows, num_partitions, hash_rate, d_out):
+        rc = self.lib.zkl_hip_hash_rows(self.ptr, C.c_void_p(d_mat), n_cols, n_rows, num_partitions, hash_rate,
+                                        C.c_void_p(d_out))
+        if rc:
+            self._err(rc)
+
+    def merkle_tree(self, d_leaves, n_leaves, d_nodes):
+        rc = self.lib.zkl_hip_merkle_tree(self.ptr, C.c_void_p(d_leaves), n_leaves, C.c_void_p(d_nodes))
+        if rc:
+            self._err(rc)
+
+    def lde(self, d_values, n_cols, n_rows, blowup, d_coeffs, d_lde):
+        rc = self.lib.zkl_hip_lde(self.ptr, C.c_void_p(d_values), n_cols, n_rows, blowup, C.c_void_p(d_coeffs),
+                                  C.c_void_p(d_lde))
+        if rc:
+            self._err(rc)
