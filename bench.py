@@ -1,0 +1,233 @@
+#!/usr/bin/env python3
+"""bench.py — segment-proofs/s of the MI355X zk-lisp segment prover.
+
+Workload (BASELINE.json configs[1] shape): one synthetic VM segment of 65,536 rows x 204
+columns ({vm, rom} layout), blowup 16, q 64, grind 16, partitions (4, 16).  One step = one
+full segment proof (trace LDE, constraint evaluation, composition, DEEP, FRI, grinding,
+queries, Proof::to_bytes) with the trace already resident in HBM.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N > 1 is launched by torch.distributed.run, one rank per GPU; each rank proves its own
+segments (weak scaling, no data-path collective).  The barrier and the
+max-over-ranks timing use torch.distributed with the gloo backend on CPU tensors: the
+prover's HIP runtime (/opt/rocm 7.2) owns the device, and loading torch's bundled ROCm
+runtime into the same process would create a second HIP runtime.
+Device synchronisation is zkl_hip_synchronize (hipDeviceSynchronize) on both sides.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "zk-lisp_amd"))
+
+METRIC = "segment-proofs/sec at 65536 rows, blowup=16; proof bytes bit-exact vs CPU ref"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MAD_PEAK_GPS = 34188.0         # measured v_mad_u64_u32 rate (profiles/r01/intbench.txt), G/s
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def perm_model(n, W=204, C=7, blowup=16, parts=None, grind=16, n_tc=193, queries=64):
+    """Algorithmic Poseidon permutation count of one segment proof (DESIGN.md §Work model)."""
+    N = n * blowup
+    if parts is None:
+        parts = 16 if n >= 1 << 20 else 8 if n >= 1 << 18 else 4 if n >= 1 << 16 else 2 if n >= 1 << 14 else 1
+    ceil = lambda a, b: -(-a // b)
+    if parts == 1:
+        row = ceil(ceil(W, 2) + 1, 10)
+        crow = ceil(ceil(C, 2) + 1, 10)
+    else:
+        ps = max(ceil(W, parts), 16)
+        np_ = ceil(W, ps)
+        row = np_ * ceil(ceil(ps, 2) + 1, 10) + ceil(np_ + 1, 10)
+        cps = max(ceil(C, parts), 16)
+        crow = ceil(ceil(C, 2) + 1, 10) + (1 if cps != C else 0)
+    n_assert = 141 * (n // 32) + 8
+    fri = 0
+    d = N
+    while d > 2 * blowup:
+        fri += d // 2 + (d // 2 - 1)
+        d //= 2
+    total = N * row + (N - 1) + N * crow + (N - 1) + fri + 2 ** grind + n_tc + n_assert + W + C + queries
+    return {"trace_rows": N * row, "total": total, "row_perms": row}
+
+
+MADS_PER_PERM = 27 * (144 + 24) * 16  # 32x32->64 multiply-adds of the schoolbook f128 products
+
+
+def cpu_baseline(log_n_sample, log_n_target):
+    """Oracle (CPU restatement of the reference algorithm), single thread, on a bounded
+    sample: one full proof of the same synthetic segment family at 2^log_n_sample rows,
+    extrapolated to 2^log_n_target rows by the permutation-count work model."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as orc
+    orc.lib()
+    orc.set_threads(1)
+    n = 1 << log_n_sample
+    t, pi, w = orc.synth_segment(0x5EED0001, log_n_sample)
+    opts = orc.default_options(w, n)
+    t0 = time.perf_counter()
+    orc.prove(t, w, n, pi, opts)
+    dt = time.perf_counter() - t0
+    ms, mt = perm_model(n), perm_model(1 << log_n_target)
+    per_target = dt * mt["total"] / ms["total"]
+    return {
+        "value": round(1.0 / per_target, 6),
+        "unit": "segment-proofs/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"oracle proof of a 2^{log_n_sample}-row synthetic segment (same options) took {dt:.1f}s "
+                   f"single-threaded; scaled x{mt['total'] / ms['total']:.1f} by the Poseidon-permutation work "
+                   f"model to a 2^{log_n_target}-row segment"),
+        "sample_seconds": round(dt, 2),
+    }
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch from the committed PMC summary (profiles/r01/pmc_traffic.json)."""
+    p = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+    try:
+        d = json.load(open(p))
+        return d.get(kernel)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--log-n", type=int, default=16)
+    ap.add_argument("--cpu-sample-log-n", type=int, default=11)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    import zkl_hip
+    ctx = zkl_hip.Context(local_rank)
+    log_n = args.log_n
+    n = 1 << log_n
+    trace, pi, W = zkl_hip.synth_vm_segment(0x5EED0001 + rank, log_n)
+    opts = zkl_hip.proof_options(W, n)
+    nbytes = W * n * 16
+    d_trace = ctx.alloc(nbytes)
+    ctx.upload(d_trace, trace, nbytes)
+    log(f"[rank {rank}] trace {W}x{n} resident in HBM; warmup {args.warmup}")
+
+    proof = None
+    for _ in range(args.warmup):
+        proof = ctx.prove_segment_device(d_trace, W, n, pi, opts)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    kacc = {}
+    barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        proof = ctx.prove_segment_device(d_trace, W, n, pi, opts)
+        for k, (ms, cnt) in ctx.kernel_times().items():
+            a = kacc.setdefault(k, [0.0, 0])
+            a[0] += ms
+            a[1] += cnt
+    ctx.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    stages = ctx.stage_times()
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank == 0:
+        value = world * args.steps / elapsed
+        # dominant kernel family and its roofline
+        dom = max(kacc.items(), key=lambda kv: kv[1][0])[0]
+        ms_tot, launches = kacc["trace_hash_rows"]
+        per_launch_ms = ms_tot / max(launches, 1)
+        N = n * 16
+        parts = opts.num_partitions
+        ps = W if parts == 1 else max(-(-W // parts), opts.hash_rate)
+        npart = -(-W // ps)
+        alg_bytes = W * N * 16 + npart * N * 16  # LDE read once + partition digests written
+        achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
+        pm = perm_model(n)
+        perms_per_launch = N * (pm["row_perms"] - (1 if parts > 1 else 0))
+        mads_per_s = perms_per_launch * MADS_PER_PERM / (per_launch_ms * 1e-3) / 1e9
+        traffic = load_traffic("hash_rows_kernel")
+        out = {
+            "metric": METRIC,
+            "value": round(value, 4),
+            "unit": "segment-proofs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f128 (u128 mod 2^128-45*2^40+1)",
+            "data": "synthetic",
+            "config": {
+                "workload": f"synthetic VM segment {n} rows x {W} cols ({{vm,rom}} layout), blowup 16, q 64, "
+                            f"grind 16, partitions ({opts.num_partitions},{opts.hash_rate}); trace resident in HBM",
+                "rows": n, "width": W, "blowup": 16, "queries": 64, "grind": 16,
+                "segments_per_gpu_per_step": 1, "parallelism": f"segments x{world} (one rank per GPU)",
+                "proof_bytes": len(proof),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "hash_rows_kernel (trace LDE row hashing, 4 partitions)",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": traffic,
+                "alg_bytes_per_launch": alg_bytes,
+                "avg_launch_ms": round(per_launch_ms, 3),
+                "note": "integer-VALU bound by construction (SURVEY 0.8); see roofline_valu",
+            },
+            "roofline_valu": {
+                "bound": "valu",
+                "achieved": round(mads_per_s, 1),
+                "peak": MAD_PEAK_GPS,
+                "unit": "G v_mad_u64_u32-equiv/s",
+                "frac": round(mads_per_s / MAD_PEAK_GPS, 4),
+                "perms_per_launch": perms_per_launch,
+            },
+            "dominant_kernel_family": dom,
+            "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kacc.items()},
+            "stage_ms_last_step": {k: round(v, 3) for k, v in stages.items()},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(args.cpu_sample_log_n, log_n)
+            except Exception as e:  # reported, never fatal for the GPU number
+                out["cpu_baseline"] = {"value": None, "error": str(e)}
+        print(json.dumps(out), flush=True)
+    ctx.free(d_trace)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -118,9 +118,19 @@ int zkl_hip_prove_segment_device(zkl_ctx* ctx, const void* d_trace, uint32_t wid
 /* Stage timings (ms) of the last proof on ctx; returns number written. */
 int zkl_hip_stage_times(const zkl_ctx* ctx, double* out_ms, int max_n);
 
-/* Per-kernel-family device time (ms, HIP events) of the last proof; names are
- * returned through *names as a static '\n'-separated list. */
-int zkl_hip_kernel_times(const zkl_ctx* ctx, double* out_ms, int max_n, const char** names);
+/* Per-kernel-family device time of the last proof, measured with HIP events on the
+ * ctx stream around each launch: out_ms[i] = summed ms, out_launches[i] = launches.
+ * *names receives a static '\n'-separated list of the family names. */
+#define ZKL_NUM_KFAMILIES 9
+int zkl_hip_kernel_times(const zkl_ctx* ctx, double* out_ms, int* out_launches, int max_n, const char** names);
+
+/* ---- device memory (the library's own HIP runtime; callers need no torch) --- */
+int zkl_hip_device_count(int* count);
+int zkl_hip_device_alloc(zkl_ctx* ctx, size_t bytes, void** d_ptr);
+int zkl_hip_device_free(zkl_ctx* ctx, void* d_ptr);
+/* kind: 1 = host->device, 2 = device->host, 3 = device->device; synchronous */
+int zkl_hip_memcpy(zkl_ctx* ctx, void* dst, const void* src, size_t bytes, int kind);
+int zkl_hip_synchronize(zkl_ctx* ctx);
 
 /* ---- reference helpers the host needs on its side ------------------------ */
 /* utils::select_partitions_for_trace (utils.rs:394-409). */

@@ -74,26 +74,55 @@ def test_full_size_deterministic(gpu_ctx):
 
 
 def test_stage_hash_rows_and_merkle(oracle, gpu_ctx):
-    import torch
     rng = random.Random(5)
     P = oracle.P
     ncols, nrows = 51, 1024
     vals = [rng.randrange(P) for _ in range(ncols * nrows)]
-    raw = b"".join(v.to_bytes(16, "little") for v in vals)
-    d_m = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
-    d_o = torch.zeros(nrows * 16, dtype=torch.uint8, device="cuda")
-    gpu_ctx.hash_rows(d_m.data_ptr(), ncols, nrows, 1, 16, d_o.data_ptr())
-    torch.cuda.synchronize()
-    got = bytes(d_o.cpu().numpy().tobytes())
+    raw = (C.c_uint8 * (16 * ncols * nrows)).from_buffer_copy(b"".join(v.to_bytes(16, "little") for v in vals))
+    d_m = gpu_ctx.alloc(len(raw))
+    d_o = gpu_ctx.alloc(nrows * 16)
+    d_nodes = gpu_ctx.alloc(2 * nrows * 16)
+    gpu_ctx.upload(d_m, raw, len(raw))
+    gpu_ctx.hash_rows(d_m, ncols, nrows, 1, 16, d_o)
+    got = gpu_ctx.download(d_o, nrows * 16)
     for r in range(0, nrows, 97):
         row = [vals[c * nrows + r] for c in range(ncols)]
         assert int.from_bytes(got[16 * r:16 * r + 16], "little") == oracle.hash_elements(row)
-    d_nodes = torch.zeros(2 * nrows * 16, dtype=torch.uint8, device="cuda")
-    gpu_ctx.merkle_tree(d_o.data_ptr(), nrows, d_nodes.data_ptr())
-    torch.cuda.synchronize()
-    nodes = bytes(d_nodes.cpu().numpy().tobytes())
-    leaves = [int.from_bytes(got[16 * i:16 * i + 16], "little") for i in range(nrows)]
-    lvl = leaves
+    gpu_ctx.merkle_tree(d_o, nrows, d_nodes)
+    nodes = gpu_ctx.download(d_nodes, 2 * nrows * 16)
+    lvl = [int.from_bytes(got[16 * i:16 * i + 16], "little") for i in range(nrows)]
     while len(lvl) > 1:
         lvl = [oracle.merge(lvl[2 * i], lvl[2 * i + 1]) for i in range(len(lvl) // 2)]
     assert int.from_bytes(nodes[16:32], "little") == lvl[0]
+    for d in (d_m, d_o, d_nodes):
+        gpu_ctx.free(d)
+
+
+def test_stage_lde_matches_oracle(oracle, gpu_ctx):
+    """zkl_hip_lde: coefficients and coset LDE (GENERATOR * <w_{16n}>) vs direct evaluation."""
+    rng = random.Random(9)
+    P = oracle.P
+    ncols, n, blow = 3, 64, 16
+    N = n * blow
+    vals = [rng.randrange(P) for _ in range(ncols * n)]
+    raw = (C.c_uint8 * (16 * ncols * n)).from_buffer_copy(b"".join(v.to_bytes(16, "little") for v in vals))
+    d_v = gpu_ctx.alloc(len(raw))
+    d_c = gpu_ctx.alloc(len(raw))
+    d_l = gpu_ctx.alloc(16 * ncols * N)
+    gpu_ctx.upload(d_v, raw, len(raw))
+    gpu_ctx.lde(d_v, ncols, n, blow, d_c, d_l)
+    coef = gpu_ctx.download(d_c, len(raw))
+    lde = gpu_ctx.download(d_l, 16 * ncols * N)
+    g = oracle.root_of_unity(6)
+    w = oracle.root_of_unity(10)
+    for c in range(ncols):
+        cs = [int.from_bytes(coef[16 * (c * n + k):16 * (c * n + k + 1)], "little") for k in range(n)]
+        for r in (0, 5, 63):
+            x = pow(g, r, P)
+            assert sum(cs[k] * pow(x, k, P) for k in range(n)) % P == vals[c * n + r]
+        for i in (0, 1, 17, N - 1):
+            x = 3 * pow(w, i, P) % P
+            want = sum(cs[k] * pow(x, k, P) for k in range(n)) % P
+            assert int.from_bytes(lde[16 * (c * N + i):16 * (c * N + i + 1)], "little") == want
+    for d in (d_v, d_c, d_l):
+        gpu_ctx.free(d)

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -126,11 +127,49 @@ struct zkl_ctx {
   // work buffers
   DBuf trace, coef, lde, parts, tree, ce, bvec, bm, clde, ctree, deep, draws, pw, oodv, asl, ast, asv, ars;
   DBuf fri_ev, fri_tree, best, gaddr, gout, flag;
-  std::vector<uint8_t> pinned_dummy;
   size_t pert_key_n = 0, pert_key_ce = 0;
+  // kernel-family timers (HIP events on `stream` around each launch group)
+  std::vector<hipEvent_t> evpool;
+  std::vector<std::pair<int, size_t>> kmarks;  // (family, index of start event; stop = +1)
+  size_t evnext = 0;
+  double kfam_ms[ZKL_NUM_KFAMILIES] = {0};
+  int kfam_n[ZKL_NUM_KFAMILIES] = {0};
 };
 
+static const char* kFamilyNames =
+    "ntt\ntrace_hash_rows\nmerkle\nconstraint_eval\ncomp_hash_rows\ndeep\nfri\ngrind\nmisc";
+enum { KF_NTT = 0, KF_TRACE_HASH, KF_MERKLE, KF_CEVAL, KF_COMP_HASH, KF_DEEP, KF_FRI, KF_GRIND, KF_MISC };
+
 namespace {
+
+struct KScope {
+  zkl_ctx* C;
+  size_t i;
+  KScope(zkl_ctx* c, int fam) : C(c) {
+    if (C->evnext + 2 > C->evpool.size()) {
+      size_t old = C->evpool.size();
+      C->evpool.resize(old + 256);
+      for (size_t k = old; k < C->evpool.size(); k++) (void)hipEventCreate(&C->evpool[k]);
+    }
+    i = C->evnext;
+    C->evnext += 2;
+    C->kmarks.push_back({fam, i});
+    (void)hipEventRecord(C->evpool[i], C->stream);
+  }
+  ~KScope() { (void)hipEventRecord(C->evpool[i + 1], C->stream); }
+};
+
+void resolve_kernel_times(zkl_ctx* C) {
+  for (int f = 0; f < ZKL_NUM_KFAMILIES; f++) { C->kfam_ms[f] = 0; C->kfam_n[f] = 0; }
+  for (auto& m : C->kmarks) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, C->evpool[m.second], C->evpool[m.second + 1]);
+    C->kfam_ms[m.first] += ms;
+    C->kfam_n[m.first]++;
+  }
+  C->kmarks.clear();
+  C->evnext = 0;
+}
 
 const char* g_global_err = "";
 thread_local std::string g_tls_err;
@@ -247,16 +286,25 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->lde.ensure((size_t)W * N * sizeof(fe));
   HIPCHECK(hipMemcpyAsync(C->coef.p, d_trace_in, (size_t)W * n * sizeof(fe),
                           trace_on_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, s));
-  launch_ntt_stages(C->coef.f(), W, n, true, 0, logn - 1, iroots, Ntab, s);  // -> n*coef, bit-reversed
-  launch_broadcast(C->coef.f(), n, 1, 0, W, n, N, C->opow_n.f(), fe_one(), false, C->lde.f(), s);
-  launch_ntt_stages(C->lde.f(), W, N, false, ilog2(B), logN - 1, roots, Ntab, s);
+  {
+    KScope k(C, KF_NTT);
+    launch_ntt_stages(C->coef.f(), W, n, true, 0, logn - 1, iroots, Ntab, s);  // -> n*coef, bit-reversed
+    launch_broadcast(C->coef.f(), n, 1, 0, W, n, N, C->opow_n.f(), fe_one(), false, C->lde.f(), s);
+    launch_ntt_stages(C->lde.f(), W, N, false, ilog2(B), logN - 1, roots, Ntab, s);
+  }
   T.mark(1);
   // ---- trace commitment (commit_to_rows + MerkleTree)
   uint32_t np_tr = o.num_partitions ? o.num_partitions : 1;
   C->parts.ensure((size_t)std::max<uint32_t>(np_tr, 1) * N * sizeof(fe) + N * sizeof(fe));
   C->tree.ensure(2 * N * sizeof(fe));
-  launch_hash_rows(C->lde.f(), W, N, o.num_partitions, o.hash_rate, C->parts.f(), C->tree.f() + N, s);
-  launch_merkle(C->tree.f(), N, s);
+  {
+    KScope k(C, KF_TRACE_HASH);
+    launch_hash_rows(C->lde.f(), W, N, o.num_partitions, o.hash_rate, C->parts.f(), C->tree.f() + N, s);
+  }
+  {
+    KScope k(C, KF_MERKLE);
+    launch_merkle(C->tree.f(), N, s);
+  }
   fe troot;
   d2h(C, &troot, C->tree.f() + 1, sizeof(fe));
   coin.reseed(troot);
@@ -266,7 +314,10 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   const size_t na = air.assertions.size();
   const size_t ndraw = (size_t)air.n_tc + na;
   C->draws.ensure((ndraw + 1024) * sizeof(fe));
-  launch_draws(coin.seed, coin.counter, ndraw, C->draws.f(), s);
+  {
+    KScope k(C, KF_MISC);
+    launch_draws(coin.seed, coin.counter, ndraw, C->draws.f(), s);
+  }
   coin.counter += ndraw;
   upload_alphas_from_device(C->draws.f(), air.n_tc, s);
 
@@ -296,11 +347,17 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->bm.ensure((size_t)(nb + 1) * ce * sizeof(fe));
   HIPCHECK(hipMemsetAsync(C->bvec.p, 0, (size_t)(nb + 1) * n * sizeof(fe), s));
   const fe* betas = C->draws.f() + air.n_tc;
-  launch_boundary_scatter((const uint32_t*)C->asl.p, (const uint32_t*)C->ast.p, betas, na, n, C->bvec.f(), s);
-  launch_boundary_w((const uint32_t*)C->ars.p, betas, C->asv.f(), n, C->bvec.f() + (size_t)nb * n, s);
-  launch_ntt_stages(C->bvec.f(), nb + 1, n, true, 0, logn - 1, roots, Ntab, s);  // forward, bit-reversed out
-  launch_broadcast(C->bvec.f(), n, 1, 0, nb + 1, n, ce, C->opow.f(), fe_one(), true, C->bm.f(), s);
-  launch_ntt_stages(C->bm.f(), nb + 1, ce, false, air.ce_blowup == 1 ? 0 : ilog2(ce / n), logce - 1, roots, Ntab, s);
+  {
+    KScope k(C, KF_CEVAL);
+    launch_boundary_scatter((const uint32_t*)C->asl.p, (const uint32_t*)C->ast.p, betas, na, n, C->bvec.f(), s);
+    launch_boundary_w((const uint32_t*)C->ars.p, betas, C->asv.f(), n, C->bvec.f() + (size_t)nb * n, s);
+  }
+  {
+    KScope k(C, KF_NTT);
+    launch_ntt_stages(C->bvec.f(), nb + 1, n, true, 0, logn - 1, roots, Ntab, s);  // forward, bit-reversed out
+    launch_broadcast(C->bvec.f(), n, 1, 0, nb + 1, n, ce, C->opow.f(), fe_one(), true, C->bm.f(), s);
+    launch_ntt_stages(C->bm.f(), nb + 1, ce, false, ilog2(ce / n), logce - 1, roots, Ntab, s);
+  }
 
   // periodic table
   if (C->pert_key_n != n || C->pert_key_ce != ce) {
@@ -327,27 +384,39 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   cp.n_bcols = nb;
   for (uint32_t u = 0; u < nb; u++) cp.bcol[u] = bcols[u];
   C->ce.ensure(ce * sizeof(fe));
-  launch_constraint_eval(C->lde.f(), roots, Ntab, C->pertab.f(), C->bm.f(), cp, C->ce.f(), s);
+  {
+    KScope k(C, KF_CEVAL);
+    launch_constraint_eval(C->lde.f(), roots, Ntab, C->pertab.f(), C->bm.f(), cp, C->ce.f(), s);
+  }
   T.mark(3);
 
   // ---- 3. composition polynomial: coset interpolation, degree check, column LDE, commit
-  launch_ntt_stages(C->ce.f(), 1, ce, true, 0, logce - 1, iroots, Ntab, s);  // ce * c_k * 3^k (bitrev)
   C->flag.ensure(16);
-  HIPCHECK(hipMemsetAsync(C->flag.p, 0, 4, s));
-  launch_check_zero_range_bitrev(C->ce.f(), ce, (size_t)Cc * n, ce, (unsigned*)C->flag.p, s);
   C->clde.ensure((size_t)Cc * N * sizeof(fe));
   const int loge = ilog2(ce / n);
   const fe inv3 = fe_inv(three), inv_ce = fe_inv(fe{ce, 0});
-  for (int j = 0; j < Cc; j++) {
-    // column j coefficient k' = chat[j n + k'] * 3^(-(j n + k')) / ce; LDE multiplies by 3^k'
-    fe mult = fe_mul(fe_pow64(inv3, (uint64_t)j * n), inv_ce);
-    launch_broadcast(C->ce.f(), 0, ce / n, bitrev_u((uint32_t)j, loge), 1, n, N, nullptr, mult, false,
-                     C->clde.f() + (size_t)j * N, s);
+  {
+    KScope k(C, KF_NTT);
+    launch_ntt_stages(C->ce.f(), 1, ce, true, 0, logce - 1, iroots, Ntab, s);  // ce * c_k * 3^k (bitrev)
+    HIPCHECK(hipMemsetAsync(C->flag.p, 0, 4, s));
+    launch_check_zero_range_bitrev(C->ce.f(), ce, (size_t)Cc * n, ce, (unsigned*)C->flag.p, s);
+    for (int j = 0; j < Cc; j++) {
+      // column j coefficient k' = chat[j n + k'] * 3^(-(j n + k')) / ce; LDE multiplies by 3^k'
+      fe mult = fe_mul(fe_pow64(inv3, (uint64_t)j * n), inv_ce);
+      launch_broadcast(C->ce.f(), 0, ce / n, bitrev_u((uint32_t)j, loge), 1, n, N, nullptr, mult, false,
+                       C->clde.f() + (size_t)j * N, s);
+    }
+    launch_ntt_stages(C->clde.f(), Cc, N, false, ilog2(B), logN - 1, roots, Ntab, s);
   }
-  launch_ntt_stages(C->clde.f(), Cc, N, false, ilog2(B), logN - 1, roots, Ntab, s);
   C->ctree.ensure(2 * N * sizeof(fe));
-  launch_hash_rows(C->clde.f(), Cc, N, o.num_partitions, o.hash_rate, C->parts.f(), C->ctree.f() + N, s);
-  launch_merkle(C->ctree.f(), N, s);
+  {
+    KScope k(C, KF_COMP_HASH);
+    launch_hash_rows(C->clde.f(), Cc, N, o.num_partitions, o.hash_rate, C->parts.f(), C->ctree.f() + N, s);
+  }
+  {
+    KScope k(C, KF_MERKLE);
+    launch_merkle(C->ctree.f(), N, s);
+  }
   unsigned bad = 0;
   d2h(C, &bad, C->flag.p, 4);
   if (bad) throw InvalidArg("constraint composition polynomial degree too large: trace does not satisfy the AIR");
@@ -367,10 +436,13 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   powers_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(fe_mul(zg, inv3), fe_one(), n, logn, pw + 3 * n);
   C->oodv.ensure(2 * ((size_t)W + Cc) * sizeof(fe));
   fe* dood = C->oodv.f();
-  launch_ood(C->coef.f(), W, n, 1, n, pw, pw + n, dood, dood + W, s);
-  for (int j = 0; j < Cc; j++)
-    launch_ood(C->ce.f() + bitrev_u((uint32_t)j, loge), 1, 0, ce / n, n, pw + 2 * n, pw + 3 * n,
-               dood + 2 * W + j, dood + 2 * W + Cc + j, s);
+  {
+    KScope k(C, KF_MISC);
+    launch_ood(C->coef.f(), W, n, 1, n, pw, pw + n, dood, dood + W, s);
+    for (int j = 0; j < Cc; j++)
+      launch_ood(C->ce.f() + bitrev_u((uint32_t)j, loge), 1, 0, ce / n, n, pw + 2 * n, pw + 3 * n,
+                 dood + 2 * W + j, dood + 2 * W + Cc + j, s);
+  }
   std::vector<fe> hood(2 * ((size_t)W + Cc));
   d2h(C, hood.data(), dood, hood.size() * sizeof(fe));
   std::vector<fe> tz(hood.begin(), hood.begin() + W), tzg(hood.begin() + W, hood.begin() + 2 * W);
@@ -400,7 +472,10 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   for (uint32_t c = 0; c < W; c++) { dp.sz = fe_add(dp.sz, fe_mul(gam[c], tz[c])); dp.szg = fe_add(dp.szg, fe_mul(gam[c], tzg[c])); }
   for (int j = 0; j < Cc; j++) { dp.sz = fe_add(dp.sz, fe_mul(gam[W + j], hz[j])); dp.szg = fe_add(dp.szg, fe_mul(gam[W + j], hzg[j])); }
   C->deep.ensure(N * sizeof(fe));
-  launch_deep(C->lde.f(), C->clde.f(), roots, Ntab, dp, C->deep.f(), s);
+  {
+    KScope k(C, KF_DEEP);
+    launch_deep(C->lde.f(), C->clde.f(), roots, Ntab, dp, C->deep.f(), s);
+  }
   T.mark(6);
 
   // ---- 6. FRI (FriProver::build_layers, folding 2, remainder degree rem_deg)
@@ -421,11 +496,18 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   for (int d = 0; d < nl; d++) {
     size_t Nd = N >> d, h = Nd / 2;
     fe* tr = C->fri_tree.f() + tr_off[d];
-    launch_fri_leaves(layer_ev(d), Nd, tr + h, s);
-    launch_merkle(tr, h, s);
+    {
+      KScope k(C, KF_FRI);
+      launch_fri_leaves(layer_ev(d), Nd, tr + h, s);
+    }
+    {
+      KScope k(C, KF_MERKLE);
+      launch_merkle(tr, h, s);
+    }
     d2h(C, &fri_roots[d], tr + 1, sizeof(fe));
     coin.reseed(fri_roots[d]);
     fe alpha = coin.draw();
+    KScope k(C, KF_FRI);
     launch_fri_fold(layer_ev(d), Nd, alpha, iroots, Ntab, layer_ev(d + 1), s);
   }
   size_t Nr = N >> nl;
@@ -458,6 +540,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     for (uint64_t base = 1; nonce == 0; base += batch, batch = std::min<uint32_t>(batch * 2, 1u << 22)) {
       unsigned long long init = ~0ull;
       HIPCHECK(hipMemcpyAsync(C->best.p, &init, 8, hipMemcpyHostToDevice, s));
+      KScope k(C, KF_GRIND);
       launch_grind(coin.seed, base, batch, o.grinding_factor, (unsigned long long*)C->best.p, s);
       unsigned long long r = 0;
       d2h(C, &r, C->best.p, 8);
@@ -569,6 +652,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   T.mark(9);
   T.mark(10);
   T.finish();
+  resolve_kernel_times(C);
   out.swap(P.v);
 }
 
@@ -667,10 +751,58 @@ int zkl_hip_stage_times(const zkl_ctx* c, double* out, int max_n) {
   return k;
 }
 
-int zkl_hip_kernel_times(const zkl_ctx* c, double* out, int max_n, const char** names) {
-  (void)c; (void)out; (void)max_n;
-  if (names) *names = "";
-  return 0;
+int zkl_hip_kernel_times(const zkl_ctx* c, double* out, int* launches, int max_n, const char** names) {
+  if (names) *names = kFamilyNames;
+  if (!c) return 0;
+  int k = std::min(max_n, ZKL_NUM_KFAMILIES);
+  for (int i = 0; i < k; i++) {
+    if (out) out[i] = c->kfam_ms[i];
+    if (launches) launches[i] = c->kfam_n[i];
+  }
+  return k;
+}
+
+int zkl_hip_device_count(int* count) {
+  if (!count) return ZKL_E_INVALID;
+  return run_guarded(nullptr, [&] { HIPCHECK(hipGetDeviceCount(count)); });
+}
+
+int zkl_hip_device_alloc(zkl_ctx* c, size_t bytes, void** d) {
+  if (!c || !d) return ZKL_E_INVALID;
+  return run_guarded(c, [&] {
+    HIPCHECK(hipSetDevice(c->device));
+    hipError_t e = hipMalloc(d, bytes);
+    if (e == hipErrorOutOfMemory) throw std::bad_alloc();
+    HIPCHECK(e);
+  });
+}
+
+int zkl_hip_device_free(zkl_ctx* c, void* d) {
+  if (!c) return ZKL_E_INVALID;
+  return run_guarded(c, [&] {
+    HIPCHECK(hipSetDevice(c->device));
+    HIPCHECK(hipFree(d));
+  });
+}
+
+int zkl_hip_memcpy(zkl_ctx* c, void* dst, const void* src, size_t bytes, int kind) {
+  if (!c || kind < 1 || kind > 3) return ZKL_E_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  return run_guarded(c, [&] {
+    HIPCHECK(hipSetDevice(c->device));
+    hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    HIPCHECK(hipMemcpyAsync(dst, src, bytes, k, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+  });
+}
+
+int zkl_hip_synchronize(zkl_ctx* c) {
+  if (!c) return ZKL_E_INVALID;
+  return run_guarded(c, [&] {
+    HIPCHECK(hipSetDevice(c->device));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    HIPCHECK(hipDeviceSynchronize());
+  });
 }
 
 void zkl_select_partitions(uint32_t w, uint32_t len, uint32_t* parts, uint32_t* rate) {

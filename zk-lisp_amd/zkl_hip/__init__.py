@@ -96,6 +96,12 @@ def load_library():
                                           P(AirPublicInputs), P(ProofOptions), P(P(C.c_uint8)), P(C.c_size_t)]
     lib.zkl_hip_prove_segment_device.argtypes = lib.zkl_hip_prove_segment.argtypes
     lib.zkl_hip_stage_times.argtypes = [C.c_void_p, P(C.c_double), C.c_int]
+    lib.zkl_hip_kernel_times.argtypes = [C.c_void_p, P(C.c_double), P(C.c_int), C.c_int, P(C.c_char_p)]
+    lib.zkl_hip_device_count.argtypes = [P(C.c_int)]
+    lib.zkl_hip_device_alloc.argtypes = [C.c_void_p, C.c_size_t, P(C.c_void_p)]
+    lib.zkl_hip_device_free.argtypes = [C.c_void_p, C.c_void_p]
+    lib.zkl_hip_memcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    lib.zkl_hip_synchronize.argtypes = [C.c_void_p]
     lib.zkl_select_partitions.argtypes = [C.c_uint32, C.c_uint32, P(C.c_uint32), P(C.c_uint32)]
     lib.zkl_synth_vm_segment.argtypes = [C.c_uint64, C.c_uint32, C.c_void_p, P(AirPublicInputs), P(C.c_uint32)]
     lib.zkl_hip_hash_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]
@@ -103,6 +109,13 @@ def load_library():
     lib.zkl_hip_lde.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]
     _lib = lib
     return lib
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = C.c_int()
+    rc = lib.zkl_hip_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
 
 
 def select_partitions_for_trace(width: int, length: int):
@@ -185,6 +198,45 @@ class Context:
         arr = (C.c_double * len(STAGE_NAMES))()
         k = self.lib.zkl_hip_stage_times(self.ptr, arr, len(STAGE_NAMES))
         return dict(zip(STAGE_NAMES[:k], list(arr)[:k]))
+
+    def kernel_times(self):
+        """{family: (ms, launches)} of the last proof, from HIP events on the ctx stream."""
+        ms = (C.c_double * 16)()
+        cnt = (C.c_int * 16)()
+        names = C.c_char_p()
+        k = self.lib.zkl_hip_kernel_times(self.ptr, ms, cnt, 16, C.byref(names))
+        fam = names.value.decode().split("\n")
+        return {fam[i]: (ms[i], cnt[i]) for i in range(k)}
+
+    # device memory owned by the library's HIP runtime
+    def alloc(self, nbytes: int) -> int:
+        p = C.c_void_p()
+        rc = self.lib.zkl_hip_device_alloc(self.ptr, nbytes, C.byref(p))
+        if rc:
+            self._err(rc)
+        return p.value
+
+    def free(self, d_ptr: int):
+        rc = self.lib.zkl_hip_device_free(self.ptr, C.c_void_p(d_ptr))
+        if rc:
+            self._err(rc)
+
+    def upload(self, d_ptr: int, host_buf, nbytes: int):
+        rc = self.lib.zkl_hip_memcpy(self.ptr, C.c_void_p(d_ptr), C.cast(host_buf, C.c_void_p), nbytes, 1)
+        if rc:
+            self._err(rc)
+
+    def download(self, d_ptr: int, nbytes: int) -> bytes:
+        buf = (C.c_uint8 * nbytes)()
+        rc = self.lib.zkl_hip_memcpy(self.ptr, C.cast(buf, C.c_void_p), C.c_void_p(d_ptr), nbytes, 2)
+        if rc:
+            self._err(rc)
+        return bytes(buf)
+
+    def synchronize(self):
+        rc = self.lib.zkl_hip_synchronize(self.ptr)
+        if rc:
+            self._err(rc)
 
     # stage entry points (device pointers)
     def hash_rows(self, d_mat, n_cols, n_rows, num_partitions, hash_rate, d_out):
