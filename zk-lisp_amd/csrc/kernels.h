@@ -14,6 +14,18 @@ struct HasherConsts {  // PoseidonHasher suite [0;32] + folded domain labels
   fe dom_elems, dom_merge, dom_many, dom_int;
 };
 void upload_hasher_consts(const HasherConsts& h, hipStream_t s);
+
+// Montgomery/26-bit-limb form of the hasher constants used by the device permutation
+// (R = 2^156 mod p; every constant stored as 5 little-endian 26-bit limbs of x*R mod p).
+struct HasherMont {
+  uint32_t mds[12][12][5];
+  uint32_t rc[27][12][5];
+  uint32_t dom[2][5];
+  uint32_t r2[5];      // R^2 mod p (converts a canonical element into Montgomery form)
+  uint32_t dfe[4][5];  // Montgomery domain labels: elements, merge, merge_many, merge_with_int
+};
+HasherMont make_hasher_mont(const HasherConsts& h);
+void upload_hasher_mont(const HasherMont& m, hipStream_t s);
 void upload_air_consts(const AirDevice& a, hipStream_t s);
 // transition composition coefficients alpha_j: copied device->constant from the draw buffer
 void upload_alphas_from_device(const fe* d_alphas, int n, hipStream_t s);

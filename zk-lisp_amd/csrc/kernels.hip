@@ -34,58 +34,190 @@ void upload_deep_coeffs(const fe* h, int n, hipStream_t s) {
 // Poseidon (poseidon/hasher.rs:173-190): 27 rounds of x^3 on all 12 lanes, dense MDS, +rc.
 // The MDS row sum is accumulated unreduced (288-bit) and reduced once per lane.
 // =====================================================================================
-// Output lanes are generated by template recursion: hipcc only partially unrolls a 12-way
-// loop this large and then indexes the state dynamically (scratch spills).
+// ---- Montgomery arithmetic on 5 x 26-bit limbs (R = 2^156) ---------------------------
+// p = 1 + 0x3F4C000*2^26 + (2^26-1)*2^52 + (2^26-1)*2^78 + (2^24-1)*2^104, and p == 1
+// (mod 2^26), so the REDC quotient digit is m = -x mod 2^26 with no multiplication.
+// Products accumulate in 64-bit columns by v_mad_u64_u32 with no carry handling: with
+// limbs < 2^28 a column holds at most 60 products < 2^56, far below 2^64.  Values are
+// kept lazily reduced (< 2^130) inside the permutation and canonicalised on output.
+__constant__ HasherMont c_hm;
+
+constexpr uint32_t M26 = 0x3FFFFFFu;
+constexpr uint32_t MP1 = 0x3F4C000u, MP2 = 0x3FFFFFFu, MP3 = 0x3FFFFFFu, MP4 = 0xFFFFFFu;
+
+__device__ __forceinline__ void to26(fe a, uint32_t l[5]) {
+  l[0] = (uint32_t)a.lo & M26;
+  l[1] = (uint32_t)(a.lo >> 26) & M26;
+  l[2] = (uint32_t)((a.lo >> 52) | (a.hi << 12)) & M26;
+  l[3] = (uint32_t)(a.hi >> 14) & M26;
+  l[4] = (uint32_t)(a.hi >> 40);
+}
+
+// col[0..9] = X (< 2^266); out = X * 2^-156 mod p, normalised limbs, value < 2^129
+__device__ __forceinline__ void redc(uint64_t col[10], uint32_t out[5]) {
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    uint32_t m = (0u - (uint32_t)col[i]) & M26;
+    col[i + 1] += (col[i] + m) >> 26;
+    col[i + 1] += (uint64_t)m * MP1;
+    col[i + 2] += (uint64_t)m * MP2;
+    col[i + 3] += (uint64_t)m * MP3;
+    col[i + 4] += (uint64_t)m * MP4;
+  }
+  uint64_t c = 0;
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    uint64_t v = col[6 + t] + c;
+    out[t] = (uint32_t)v & M26;
+    c = v >> 26;
+  }
+  out[4] = (uint32_t)c;
+}
+
+__device__ __forceinline__ void mac5(const uint32_t a[5], const uint32_t b[5], uint64_t col[10]) {
+#pragma unroll
+  for (int u = 0; u < 5; u++)
+#pragma unroll
+    for (int v = 0; v < 5; v++) col[u + v] += (uint64_t)a[u] * b[v];
+}
+
+__device__ __forceinline__ void mont_mul(const uint32_t a[5], const uint32_t b[5], uint32_t out[5]) {
+  uint64_t col[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  mac5(a, b, col);
+  redc(col, out);
+}
+
+__device__ __forceinline__ void mont_cube(const uint32_t a[5], uint32_t out[5]) {
+  uint64_t col[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t d[5];
+#pragma unroll
+  for (int u = 0; u < 5; u++) d[u] = a[u] << 1;
+#pragma unroll
+  for (int u = 0; u < 5; u++) {
+    col[2 * u] += (uint64_t)a[u] * a[u];
+#pragma unroll
+    for (int v = u + 1; v < 5; v++) col[u + v] += (uint64_t)d[u] * a[v];
+  }
+  uint32_t sq[5];
+  redc(col, sq);
+  mont_mul(sq, a, out);
+}
+
+__device__ __forceinline__ void to_mont(fe a, uint32_t out[5]) {
+  uint32_t l[5];
+  to26(a, l);
+  mont_mul(l, c_hm.r2, out);
+}
+
+__device__ __forceinline__ fe from_mont(const uint32_t a[5]) {
+  uint64_t col[10] = {a[0], a[1], a[2], a[3], a[4], 0, 0, 0, 0, 0};
+  uint32_t l[5];
+  redc(col, l);  // < p + 1
+  fe r;
+  r.lo = (uint64_t)l[0] | ((uint64_t)l[1] << 26) | ((uint64_t)l[2] << 52);
+  r.hi = ((uint64_t)l[2] >> 12) | ((uint64_t)l[3] << 14) | ((uint64_t)l[4] << 40);
+  if (r.hi == P_HI && r.lo >= P_LO) r = fe{r.lo - P_LO, 0};
+  return r;
+}
+
+// Output lanes by template recursion: hipcc only partially unrolls a 12-way loop this
+// large and then indexes the state dynamically (scratch spills).
 template <int I>
 struct MdsRow {
-  static __device__ __forceinline__ void run(const fe* c, fe* st, int r) {
-    uint32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  static __device__ __forceinline__ void run(const uint32_t (*c)[5], uint32_t (*st)[5], int r) {
+    uint64_t col[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 12; k++) mul_acc(c_h.mds[I * 12 + k], c[k], acc);
-    st[I] = fe_add(reduce288(acc), c_h.rc[r * 12 + I]);
+    for (int k = 0; k < 12; k++) mac5(c[k], c_hm.mds[I][k], col);
+    redc(col, st[I]);
+#pragma unroll
+    for (int j = 0; j < 5; j++) st[I][j] += c_hm.rc[r][I][j];
     MdsRow<I + 1>::run(c, st, r);
   }
 };
 template <>
 struct MdsRow<12> {
-  static __device__ __forceinline__ void run(const fe*, fe*, int) {}
+  static __device__ __forceinline__ void run(const uint32_t (*)[5], uint32_t (*)[5], int) {}
 };
 
-__device__ __forceinline__ void permute(fe st[12]) {
+// Poseidon permutation (poseidon/hasher.rs:173-190): 27 rounds of x^3 on all 12 lanes,
+// dense 12x12 MDS, + round constants; state in Montgomery form.
+__device__ __forceinline__ void permute(uint32_t st[12][5]) {
 #pragma unroll 1
   for (int r = 0; r < 27; r++) {
-    fe c[12];
+    uint32_t c[12][5];
 #pragma unroll
-    for (int i = 0; i < 12; i++) c[i] = fe_cube(st[i]);
+    for (int i = 0; i < 12; i++) mont_cube(st[i], c[i]);
     MdsRow<0>::run(c, st, r);
   }
 }
 
+enum { DOM_ELEMS = 0, DOM_MERGE = 1, DOM_MANY = 2, DOM_INT = 3 };
+
 // ro_bytes_sponge_custom_rounds (hasher.rs:144-231) over pre-folded 32-byte chunks:
 // absorb dom_fe then nmsg messages at rate 10, permute when the rate fills and once at the
 // end if partial.  Lanes are walked in groups of 10 so register indices stay static.
-template <class Loader>
-__device__ __forceinline__ fe sponge(fe dom_fe, int nmsg, Loader ld) {
-  fe st[12];
+template <int D, class Loader>
+__device__ __forceinline__ fe sponge(int nmsg, Loader ld) {
+  uint32_t st[12][5];
 #pragma unroll
-  for (int i = 0; i < 12; i++) st[i] = fe_zero();
-  st[10] = c_h.dom[0];
-  st[11] = c_h.dom[1];
-  st[0] = dom_fe;
+  for (int i = 0; i < 12; i++)
+#pragma unroll
+    for (int j = 0; j < 5; j++) st[i][j] = 0;
+#pragma unroll
+  for (int j = 0; j < 5; j++) {
+    st[0][j] = c_hm.dfe[D][j];
+    st[10][j] = c_hm.dom[0][j];
+    st[11][j] = c_hm.dom[1][j];
+  }
   const int T = nmsg + 1;
   for (int g = 0; g * 10 < T; g++) {
 #pragma unroll
     for (int l = 0; l < 10; l++) {
       int idx = g * 10 + l;
-      if (idx >= 1 && idx < T) st[l] = fe_add(st[l], ld(idx - 1));
+      if (idx >= 1 && idx < T) {
+        uint32_t m[5];
+        to_mont(ld(idx - 1), m);
+#pragma unroll
+        for (int j = 0; j < 5; j++) st[l][j] += m[j];
+      }
     }
     permute(st);
   }
-  return st[0];
+  return from_mont(st[0]);
 }
 
 __device__ __forceinline__ fe merge2(fe a, fe b) {
-  return sponge(c_h.dom_merge, 2, [&](int j) { return j == 0 ? a : b; });
+  return sponge<DOM_MERGE>(2, [&](int j) { return j == 0 ? a : b; });
+}
+
+static void limbs26(fe a, uint32_t l[5]) {
+  l[0] = (uint32_t)a.lo & M26;
+  l[1] = (uint32_t)(a.lo >> 26) & M26;
+  l[2] = (uint32_t)((a.lo >> 52) | (a.hi << 12)) & M26;
+  l[3] = (uint32_t)(a.hi >> 14) & M26;
+  l[4] = (uint32_t)(a.hi >> 40);
+}
+
+HasherMont make_hasher_mont(const HasherConsts& h) {
+  HasherMont m{};
+  fe R = fe_pow64(fe{2, 0}, 156);  // 2^156 mod p
+  auto mont = [&](fe x, uint32_t out[5]) { limbs26(fe_mul(x, R), out); };
+  for (int i = 0; i < 12; i++)
+    for (int k = 0; k < 12; k++) mont(h.mds[i * 12 + k], m.mds[i][k]);
+  for (int r = 0; r < 27; r++)
+    for (int i = 0; i < 12; i++) mont(h.rc[r * 12 + i], m.rc[r][i]);
+  mont(h.dom[0], m.dom[0]);
+  mont(h.dom[1], m.dom[1]);
+  limbs26(fe_mul(R, R), m.r2);
+  mont(h.dom_elems, m.dfe[DOM_ELEMS]);
+  mont(h.dom_merge, m.dfe[DOM_MERGE]);
+  mont(h.dom_many, m.dfe[DOM_MANY]);
+  mont(h.dom_int, m.dfe[DOM_INT]);
+  return m;
+}
+
+void upload_hasher_mont(const HasherMont& m, hipStream_t s) {
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_hm), &m, sizeof m, 0, hipMemcpyHostToDevice, s);
 }
 
 // ---- row hashing: one thread per (row, partition); column-major reads are coalesced
@@ -96,7 +228,7 @@ __global__ __launch_bounds__(256) void hash_rows_kernel(const fe* __restrict__ M
   uint32_t c0 = blockIdx.y * psize;
   uint32_t len = min(psize, ncols - c0);
   const fe* base = M + (size_t)c0 * nrows + row;
-  fe d = sponge(c_h.dom_elems, (int)((len + 1) / 2), [&](int j) {
+  fe d = sponge<DOM_ELEMS>((int)((len + 1) / 2), [&](int j) {
     fe a = base[(size_t)(2 * j) * nrows];
     fe b = (2u * j + 1 < len) ? base[(size_t)(2 * j + 1) * nrows] : fe_zero();
     return fold_pair(a, b);
@@ -108,7 +240,7 @@ __global__ __launch_bounds__(256) void merge_parts_kernel(const fe* __restrict__
                                                           fe* __restrict__ out) {
   size_t row = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= nrows) return;
-  out[row] = sponge(c_h.dom_many, (int)np, [&](int j) { return parts[(size_t)j * nrows + row]; });
+  out[row] = sponge<DOM_MANY>((int)np, [&](int j) { return parts[(size_t)j * nrows + row]; });
 }
 
 __global__ __launch_bounds__(256) void merkle_level_kernel(fe* nodes, size_t lvl) {
@@ -121,7 +253,7 @@ __global__ __launch_bounds__(256) void draw_kernel(fe seed, uint64_t base, size_
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= k) return;
   uint64_t ctr = base + 1 + i;
-  out[i] = sponge(c_h.dom_int, 2, [&](int j) { return j == 0 ? seed : fe{ctr, 0}; });
+  out[i] = sponge<DOM_INT>(2, [&](int j) { return j == 0 ? seed : fe{ctr, 0}; });
 }
 
 __global__ __launch_bounds__(256) void grind_kernel(fe seed, uint64_t base, uint32_t count, uint32_t bits,
@@ -129,7 +261,7 @@ __global__ __launch_bounds__(256) void grind_kernel(fe seed, uint64_t base, uint
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   uint64_t nonce = base + i;
-  fe h = sponge(c_h.dom_int, 2, [&](int j) { return j == 0 ? seed : fe{nonce, 0}; });
+  fe h = sponge<DOM_INT>(2, [&](int j) { return j == 0 ? seed : fe{nonce, 0}; });
   uint32_t tz = h.lo ? (uint32_t)__builtin_ctzll(h.lo) : 64u;
   if (tz >= bits) atomicMin(best, (unsigned long long)nonce);
 }
@@ -627,7 +759,7 @@ __global__ __launch_bounds__(256) void fri_leaf_kernel(const fe* ev, size_t half
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= half) return;
   fe m = fold_pair(ev[i], ev[i + half]);
-  leaves[i] = sponge(c_h.dom_elems, 1, [&](int) { return m; });
+  leaves[i] = sponge<DOM_ELEMS>(1, [&](int) { return m; });
 }
 void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s) {
   size_t h = Nd / 2;

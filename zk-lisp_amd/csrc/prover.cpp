@@ -180,6 +180,23 @@ void set_err(zkl_ctx* c, const std::string& m) {
   g_global_err = g_tls_err.c_str();
 }
 
+// PoseidonHasher constants (suite [0;32]) in both device forms
+void upload_hasher(hipStream_t s) {
+  static HasherConsts hc;
+  static HasherMont hm;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const Hasher& H = hasher();
+    for (int i = 0; i < 144; i++) hc.mds[i] = H.suite.mds[i / 12][i % 12];
+    for (int r = 0; r < 27; r++) for (int l = 0; l < 12; l++) hc.rc[r * 12 + l] = H.suite.rc[r][l];
+    hc.dom[0] = H.suite.dom[0]; hc.dom[1] = H.suite.dom[1];
+    hc.dom_elems = H.dom_elems; hc.dom_merge = H.dom_merge; hc.dom_many = H.dom_many; hc.dom_int = H.dom_int;
+    hm = make_hasher_mont(hc);
+  });
+  upload_hasher_consts(hc, s);
+  upload_hasher_mont(hm, s);
+}
+
 void ensure_tables(zkl_ctx* C, size_t n, size_t N) {
   hipStream_t s = C->stream;
   if (C->tab_N < N) {
@@ -261,12 +278,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   const fe g = root_of_unity(logn), three{3, 0};
   const Hasher& H = hasher();
 
-  HasherConsts hc{};
-  for (int i = 0; i < 144; i++) hc.mds[i] = H.suite.mds[i / 12][i % 12];
-  for (int r = 0; r < 27; r++) for (int l = 0; l < 12; l++) hc.rc[r * 12 + l] = H.suite.rc[r][l];
-  hc.dom[0] = H.suite.dom[0]; hc.dom[1] = H.suite.dom[1];
-  hc.dom_elems = H.dom_elems; hc.dom_merge = H.dom_merge; hc.dom_many = H.dom_many; hc.dom_int = H.dom_int;
-  upload_hasher_consts(hc, s);
+  upload_hasher(s);
   upload_air_consts(air.dev, s);
   ensure_tables(C, n, N);
   const fe* roots = C->roots.f();
@@ -815,13 +827,7 @@ int zkl_hip_hash_rows(zkl_ctx* c, const void* d_m, uint32_t nc, uint32_t nr, uin
   std::lock_guard<std::mutex> lk(c->mu);
   return run_guarded(c, [&] {
     HIPCHECK(hipSetDevice(c->device));
-    const Hasher& H = hasher();
-    HasherConsts hc{};
-    for (int i = 0; i < 144; i++) hc.mds[i] = H.suite.mds[i / 12][i % 12];
-    for (int r = 0; r < 27; r++) for (int l = 0; l < 12; l++) hc.rc[r * 12 + l] = H.suite.rc[r][l];
-    hc.dom[0] = H.suite.dom[0]; hc.dom[1] = H.suite.dom[1];
-    hc.dom_elems = H.dom_elems; hc.dom_merge = H.dom_merge; hc.dom_many = H.dom_many; hc.dom_int = H.dom_int;
-    upload_hasher_consts(hc, c->stream);
+    upload_hasher(c->stream);
     c->parts.ensure((size_t)std::max<uint32_t>(np, 1) * nr * sizeof(fe) + 16);
     launch_hash_rows((const fe*)d_m, nc, nr, np, rate, c->parts.f(), (fe*)d_out, c->stream);
     HIPCHECK(hipStreamSynchronize(c->stream));
@@ -833,13 +839,7 @@ int zkl_hip_merkle_tree(zkl_ctx* c, const void* d_leaves, uint32_t n, void* d_no
   std::lock_guard<std::mutex> lk(c->mu);
   return run_guarded(c, [&] {
     HIPCHECK(hipSetDevice(c->device));
-    const Hasher& H = hasher();
-    HasherConsts hc{};
-    for (int i = 0; i < 144; i++) hc.mds[i] = H.suite.mds[i / 12][i % 12];
-    for (int r = 0; r < 27; r++) for (int l = 0; l < 12; l++) hc.rc[r * 12 + l] = H.suite.rc[r][l];
-    hc.dom[0] = H.suite.dom[0]; hc.dom[1] = H.suite.dom[1];
-    hc.dom_elems = H.dom_elems; hc.dom_merge = H.dom_merge; hc.dom_many = H.dom_many; hc.dom_int = H.dom_int;
-    upload_hasher_consts(hc, c->stream);
+    upload_hasher(c->stream);
     HIPCHECK(hipMemcpyAsync((fe*)d_nodes + n, d_leaves, (size_t)n * sizeof(fe), hipMemcpyDeviceToDevice, c->stream));
     HIPCHECK(hipMemsetAsync(d_nodes, 0, sizeof(fe), c->stream));
     launch_merkle((fe*)d_nodes, n, c->stream);
