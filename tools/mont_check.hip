@@ -1,0 +1,64 @@
+// Host-side check of the device Montgomery helpers in kernels.hip (REDC, mont_mul,
+// mont_cube) against u128 reference arithmetic.  Build: tools/mont_check.sh
+#include "../zk-lisp_amd/csrc/kernels.hip"
+#include <cstdio>
+#include <random>
+using namespace zkl;
+static fe from26(const uint32_t l[5]) {  // value may exceed p: reduce via u128 mod
+  unsigned __int128 v = 0;
+  // value < 2^130: accumulate as (hi part) carefully
+  unsigned __int128 lo = (unsigned __int128)l[0] + ((unsigned __int128)l[1] << 26) + ((unsigned __int128)l[2] << 52) +
+                         ((unsigned __int128)l[3] << 78);
+  unsigned __int128 top = (unsigned __int128)l[4];  // * 2^104
+  unsigned __int128 P = ((unsigned __int128)P_HI << 64) | P_LO;
+  // top * 2^104 mod p
+  unsigned __int128 t = top << 24;  // top*2^24 < 2^50
+  // (t * 2^80) mod p computed by repeated doubling
+  for (int i = 0; i < 80; i++) { t = (t >= P - t) ? t - (P - t) : t + t; }
+  lo %= P;
+  v = (lo >= P - t) ? lo - (P - t) : lo + t;
+  return fe{(uint64_t)v, (uint64_t)(v >> 64)};
+}
+int main() {
+  std::mt19937_64 rng(7);
+  fe R = fe_pow64(fe{2, 0}, 156), Rinv = fe_inv(R);
+  int bad = 0;
+  for (int it = 0; it < 200000; it++) {
+    fe a{rng(), rng() >> (it % 3)}, b{rng(), rng() >> (it % 5)};
+    if (a.hi == P_HI && a.lo >= P_LO) a.hi--;
+    if (b.hi == P_HI && b.lo >= P_LO) b.hi--;
+    uint32_t la[5], lb[5], lo[5], lc[5];
+    to26(a, la); to26(b, lb);
+    if (it & 1) { for (int j = 0; j < 5; j++) { la[j] += (uint32_t)(rng() & 0x3FFFFFF); } }  // lazy limbs < 2^27
+    fe av = from26(la);
+    mont_mul(la, lb, lo);
+    fe got = from26(lo), want = fe_mul(fe_mul(av, b), Rinv);
+    unsigned __int128 gv = ((unsigned __int128)0);
+    (void)gv;
+    bool lim = true;
+    for (int j = 0; j < 4; j++) lim &= lo[j] < (1u << 26);
+    lim &= lo[4] < (1u << 26);
+    if (!fe_eq(got, want) || !lim) { if (bad++ < 5) printf("mul mismatch it=%d\n", it); }
+    mont_cube(la, lc);
+    fe wantc = fe_mul(fe_mul(fe_mul(av, av), av), fe_mul(Rinv, Rinv));
+    if (!fe_eq(from26(lc), wantc)) { if (bad++ < 5) printf("cube mismatch it=%d\n", it); }
+  }
+  // 12-term accumulated products (MDS shape), max-size limbs
+  for (int it = 0; it < 50000; it++) {
+    uint64_t col[10] = {0};
+    fe acc = fe_zero();
+    for (int k = 0; k < 12; k++) {
+      uint32_t x[5], y[5];
+      for (int j = 0; j < 5; j++) { x[j] = (uint32_t)(rng() & 0x3FFFFFF); y[j] = (uint32_t)(rng() & 0x3FFFFFF); }
+      x[4] &= 0x1FFFFFF; y[4] &= 0xFFFFFF;
+      if (it == 0) { for (int j = 0; j < 5; j++) { x[j] = 0x3FFFFFF; } x[4] = 0x1FFFFFF; y[0]=y[1]=y[2]=y[3]=0x3FFFFFF; y[4]=0xFFFFFF; }
+      mac5(x, y, col);
+      acc = fe_add(acc, fe_mul(from26(x), from26(y)));
+    }
+    uint32_t o[5];
+    redc(col, o);
+    if (!fe_eq(from26(o), fe_mul(acc, Rinv))) { if (bad++ < 10) printf("mds mismatch it=%d\n", it); }
+  }
+  printf(bad ? "FAIL %d\n" : "OK\n", bad);
+  return bad != 0;
+}

@@ -43,9 +43,8 @@ void upload_deep_coeffs(const fe* h, int n, hipStream_t s) {
 __constant__ HasherMont c_hm;
 
 constexpr uint32_t M26 = 0x3FFFFFFu;
-constexpr uint32_t MP1 = 0x3F4C000u, MP2 = 0x3FFFFFFu, MP3 = 0x3FFFFFFu, MP4 = 0xFFFFFFu;
 
-__device__ __forceinline__ void to26(fe a, uint32_t l[5]) {
+__host__ __device__ __forceinline__ void to26(fe a, uint32_t l[5]) {
   l[0] = (uint32_t)a.lo & M26;
   l[1] = (uint32_t)(a.lo >> 26) & M26;
   l[2] = (uint32_t)((a.lo >> 52) | (a.hi << 12)) & M26;
@@ -53,41 +52,59 @@ __device__ __forceinline__ void to26(fe a, uint32_t l[5]) {
   l[4] = (uint32_t)(a.hi >> 40);
 }
 
-// col[0..9] = X (< 2^266); out = X * 2^-156 mod p, normalised limbs, value < 2^129
-__device__ __forceinline__ void redc(uint64_t col[10], uint32_t out[5]) {
+// col[0..9] = X (< 2^262, columns < 2^62); out = X * 2^-156 mod p + (0 or p): normalised
+// 26-bit limbs of a value in (0, 2^130).  p = 1 + 45*2^14*2^26 ... written in columns is
+// p = 2^0 + 737280*2^26 - 2^24*2^104 (... - 45*2^40 + 2^128), so removing m*p*2^(26i)
+// from X touches only three columns: col_i -= m (exact: m = col_i mod 2^26, the rest
+// carries), col_{i+1} += 737280*m, col_{i+4} -= 2^24*m.  Columns are signed; adding
+// p*2^156 up front (col_6 += 1, col_7 -= 737280, col_9 += 2^50) keeps the result positive.
+__host__ __device__ __forceinline__ void redc(uint64_t colu[10], uint32_t out[5]) {
+  int64_t col[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) col[i] = (int64_t)colu[i];
+  col[6] += 1;
+  col[7] -= 737280;
+  col[9] += (int64_t)1 << 50;
+  // opaque copies of the two reduction constants: keeps -2^24*m a single v_mad_i64_i32
+  // instead of a 64-bit shift + subtract
+  int32_t kneg = -16777216;
+  uint32_t k45 = 737280u;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+s"(kneg), "+s"(k45));
+#endif
 #pragma unroll
   for (int i = 0; i < 6; i++) {
-    uint32_t m = (0u - (uint32_t)col[i]) & M26;
-    col[i + 1] += (col[i] + m) >> 26;
-    col[i + 1] += (uint64_t)m * MP1;
-    col[i + 2] += (uint64_t)m * MP2;
-    col[i + 3] += (uint64_t)m * MP3;
-    col[i + 4] += (uint64_t)m * MP4;
+    const uint32_t m = (uint32_t)col[i] & M26;
+    col[i + 1] += col[i] >> 26;
+    col[i + 1] += (int64_t)((uint64_t)m * k45);
+    col[i + 4] += (int64_t)(int32_t)m * (int64_t)kneg;
   }
-  uint64_t c = 0;
+  int64_t c = 0;
 #pragma unroll
-  for (int t = 0; t < 4; t++) {
-    uint64_t v = col[6 + t] + c;
+  for (int t = 0; t < 3; t++) {
+    const int64_t v = col[6 + t] + c;
     out[t] = (uint32_t)v & M26;
     c = v >> 26;
   }
-  out[4] = (uint32_t)c;
+  const int64_t v = col[9] + c;
+  out[3] = (uint32_t)v & M26;
+  out[4] = (uint32_t)(v >> 26);
 }
 
-__device__ __forceinline__ void mac5(const uint32_t a[5], const uint32_t b[5], uint64_t col[10]) {
+__host__ __device__ __forceinline__ void mac5(const uint32_t a[5], const uint32_t b[5], uint64_t col[10]) {
 #pragma unroll
   for (int u = 0; u < 5; u++)
 #pragma unroll
     for (int v = 0; v < 5; v++) col[u + v] += (uint64_t)a[u] * b[v];
 }
 
-__device__ __forceinline__ void mont_mul(const uint32_t a[5], const uint32_t b[5], uint32_t out[5]) {
+__host__ __device__ __forceinline__ void mont_mul(const uint32_t a[5], const uint32_t b[5], uint32_t out[5]) {
   uint64_t col[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   mac5(a, b, col);
   redc(col, out);
 }
 
-__device__ __forceinline__ void mont_cube(const uint32_t a[5], uint32_t out[5]) {
+__host__ __device__ __forceinline__ void mont_cube(const uint32_t a[5], uint32_t out[5]) {
   uint64_t col[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t d[5];
 #pragma unroll
@@ -120,75 +137,7 @@ __device__ __forceinline__ fe from_mont(const uint32_t a[5]) {
   return r;
 }
 
-// Output lanes by template recursion: hipcc only partially unrolls a 12-way loop this
-// large and then indexes the state dynamically (scratch spills).
-template <int I>
-struct MdsRow {
-  static __device__ __forceinline__ void run(const uint32_t (*c)[5], uint32_t (*st)[5], int r) {
-    uint64_t col[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 12; k++) mac5(c[k], c_hm.mds[I][k], col);
-    redc(col, st[I]);
-#pragma unroll
-    for (int j = 0; j < 5; j++) st[I][j] += c_hm.rc[r][I][j];
-    MdsRow<I + 1>::run(c, st, r);
-  }
-};
-template <>
-struct MdsRow<12> {
-  static __device__ __forceinline__ void run(const uint32_t (*)[5], uint32_t (*)[5], int) {}
-};
-
-// Poseidon permutation (poseidon/hasher.rs:173-190): 27 rounds of x^3 on all 12 lanes,
-// dense 12x12 MDS, + round constants; state in Montgomery form.
-__device__ __forceinline__ void permute(uint32_t st[12][5]) {
-#pragma unroll 1
-  for (int r = 0; r < 27; r++) {
-    uint32_t c[12][5];
-#pragma unroll
-    for (int i = 0; i < 12; i++) mont_cube(st[i], c[i]);
-    MdsRow<0>::run(c, st, r);
-  }
-}
-
 enum { DOM_ELEMS = 0, DOM_MERGE = 1, DOM_MANY = 2, DOM_INT = 3 };
-
-// ro_bytes_sponge_custom_rounds (hasher.rs:144-231) over pre-folded 32-byte chunks:
-// absorb dom_fe then nmsg messages at rate 10, permute when the rate fills and once at the
-// end if partial.  Lanes are walked in groups of 10 so register indices stay static.
-template <int D, class Loader>
-__device__ __forceinline__ fe sponge(int nmsg, Loader ld) {
-  uint32_t st[12][5];
-#pragma unroll
-  for (int i = 0; i < 12; i++)
-#pragma unroll
-    for (int j = 0; j < 5; j++) st[i][j] = 0;
-#pragma unroll
-  for (int j = 0; j < 5; j++) {
-    st[0][j] = c_hm.dfe[D][j];
-    st[10][j] = c_hm.dom[0][j];
-    st[11][j] = c_hm.dom[1][j];
-  }
-  const int T = nmsg + 1;
-  for (int g = 0; g * 10 < T; g++) {
-#pragma unroll
-    for (int l = 0; l < 10; l++) {
-      int idx = g * 10 + l;
-      if (idx >= 1 && idx < T) {
-        uint32_t m[5];
-        to_mont(ld(idx - 1), m);
-#pragma unroll
-        for (int j = 0; j < 5; j++) st[l][j] += m[j];
-      }
-    }
-    permute(st);
-  }
-  return from_mont(st[0]);
-}
-
-__device__ __forceinline__ fe merge2(fe a, fe b) {
-  return sponge<DOM_MERGE>(2, [&](int j) { return j == 0 ? a : b; });
-}
 
 static void limbs26(fe a, uint32_t l[5]) {
   l[0] = (uint32_t)a.lo & M26;
@@ -220,80 +169,211 @@ void upload_hasher_mont(const HasherMont& m, hipStream_t s) {
   (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_hm), &m, sizeof m, 0, hipMemcpyHostToDevice, s);
 }
 
-// ---- row hashing: one thread per (row, partition); column-major reads are coalesced
-__global__ __launch_bounds__(256) void hash_rows_kernel(const fe* __restrict__ M, uint32_t ncols, size_t nrows,
+// ---- lane-group permutation ------------------------------------------------------------
+// One Poseidon state is held by 12 lanes of a wave: lane j owns s_j (5 limbs) and row j of
+// the MDS matrix (60 VGPRs, loaded once).  A round is: cube own lane -> publish it in LDS
+// -> read all 12 cubes of the group -> own MDS row sum -> REDC -> +rc.  A wave holds five
+// states (lanes 0..59); lanes 60..63 form a partial sixth group whose results are unused.
+// Compared with one state per lane this keeps the MDS constants in registers instead of
+// re-streaming them through SGPRs, and cuts the latency of one permutation twelve-fold,
+// which is what bounds the upper Merkle levels and the FRI layers.
+constexpr int PG_LANES = 12;
+constexpr int PG_PER_WAVE = 5;
+constexpr int PG_WAVE_WORDS = 6 * 60;  // six groups x (5 limbs x 12 lanes)
+
+struct PGroup {
+  uint32_t m[12][5];  // MDS row j (Montgomery)
+  uint32_t* x;        // this group's exchange area: x[limb * 12 + lane]
+  int j;              // lane within the group
+  int g;              // group within the wave (5 = the partial group)
+};
+
+__device__ __forceinline__ void pg_init(PGroup& P, uint32_t* lds) {
+  const int lane = (int)(threadIdx.x & 63);
+  P.g = lane / PG_LANES;
+  P.j = lane - PG_LANES * P.g;
+  P.x = lds + (threadIdx.x >> 6) * PG_WAVE_WORDS + P.g * 60;
+#pragma unroll
+  for (int k = 0; k < 12; k++)
+#pragma unroll
+    for (int l = 0; l < 5; l++) P.m[k][l] = c_hm.mds[P.j][k][l];
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Poseidon permutation (poseidon/hasher.rs:173-190): 27 rounds of x^3 on all 12 lanes,
+// dense 12x12 MDS, + round constants.  s = this lane's state element (Montgomery).
+__device__ __forceinline__ void pg_permute(PGroup& P, uint32_t s[5]) {
+  const uint4* xv = reinterpret_cast<const uint4*>(P.x);
+  const uint32_t* rcp = &c_hm.rc[0][P.j][0];
+#pragma unroll 1
+  for (int r = 0; r < 27; r++, rcp += 60) {
+    uint32_t rc[5];  // issued early; consumed after the MDS row sum
+#pragma unroll
+    for (int l = 0; l < 5; l++) rc[l] = rcp[l];
+    uint32_t t[5];
+    mont_cube(s, t);
+#pragma unroll
+    for (int l = 0; l < 5; l++) P.x[l * 12 + P.j] = t[l];
+    wave_sync();
+    uint4 v[15];  // all twelve cubes of the group, limb-major: v[l*3+q] = limb l of lanes 4q..4q+3
+#pragma unroll
+    for (int i = 0; i < 15; i++) v[i] = xv[i];
+    __builtin_amdgcn_wave_barrier();
+    uint64_t col[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      uint32_t a0[5] = {v[q].x, v[3 + q].x, v[6 + q].x, v[9 + q].x, v[12 + q].x};
+      uint32_t a1[5] = {v[q].y, v[3 + q].y, v[6 + q].y, v[9 + q].y, v[12 + q].y};
+      uint32_t a2[5] = {v[q].z, v[3 + q].z, v[6 + q].z, v[9 + q].z, v[12 + q].z};
+      uint32_t a3[5] = {v[q].w, v[3 + q].w, v[6 + q].w, v[9 + q].w, v[12 + q].w};
+      mac5(a0, P.m[4 * q + 0], col);
+      mac5(a1, P.m[4 * q + 1], col);
+      mac5(a2, P.m[4 * q + 2], col);
+      mac5(a3, P.m[4 * q + 3], col);
+    }
+    redc(col, s);
+#pragma unroll
+    for (int l = 0; l < 5; l++) s[l] += rc[l];
+  }
+}
+
+// ro_bytes_sponge_custom_rounds (hasher.rs:144-231) over pre-folded 32-byte chunks: the
+// stream [dom_fe, msg_0, .., msg_{n-1}] is added into lanes 0..9 ten at a time, permuting
+// after each block (the last one possibly partial).  nmsg must be uniform within a group;
+// ld(i) is called only by the lane that absorbs message i, and only when live.  Returns
+// the digest value (state[0]) in lane 0 of the group.
+template <int D, class Loader>
+__device__ __forceinline__ fe pg_sponge(PGroup& P, bool live, int nmsg, Loader ld) {
+  uint32_t s[5];
+#pragma unroll
+  for (int l = 0; l < 5; l++)
+    s[l] = P.j == 0 ? c_hm.dfe[D][l] : P.j == 10 ? c_hm.dom[0][l] : P.j == 11 ? c_hm.dom[1][l] : 0u;
+  const int T = nmsg + 1;
+  for (int b = 0; b * 10 < T; b++) {
+    const int idx = b * 10 + P.j;
+    if (live && P.j < 10 && idx >= 1 && idx < T) {
+      uint32_t m[5];
+      to_mont(ld(idx - 1), m);
+#pragma unroll
+      for (int l = 0; l < 5; l++) s[l] += m[l];
+    }
+    pg_permute(P, s);
+  }
+  return from_mont(s);
+}
+
+// broadcast lane `src` of this thread's group to every lane of the group
+__device__ __forceinline__ fe pg_bcast(const PGroup& P, fe v, int src) {
+  const int from = (int)(threadIdx.x & 63) - P.j + src;
+  fe r;
+  r.lo = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v.lo >> 32), from) << 32) | (uint32_t)__shfl((int)(uint32_t)v.lo, from);
+  r.hi = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v.hi >> 32), from) << 32) | (uint32_t)__shfl((int)(uint32_t)v.hi, from);
+  return r;
+}
+
+// Occupancy target of the lane-group kernels: 2 waves/SIMD lets the scheduler batch the 15
+// LDS reads of a round; 3 forces them to serialise on a shared register window.
+#ifndef PG_WAVES
+#define PG_WAVES 2
+#endif
+#define PG_KERNEL __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PG_WAVES, PG_WAVES)))
+
+#define PG_SETUP()                                          \
+  __shared__ __align__(16) uint32_t pg_lds[4 * PG_WAVE_WORDS]; \
+  PGroup P;                                                 \
+  pg_init(P, pg_lds);                                       \
+  const size_t item = ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * PG_PER_WAVE + (size_t)P.g;
+
+static inline unsigned pg_blocks(size_t items) {
+  const size_t per = 4 * PG_PER_WAVE;
+  return (unsigned)((items + per - 1) / per);
+}
+
+// ---- row hashing (Winterfell partitioned row hash): one group per row.  The row's
+// partitions are hashed one after another (hash_elements over psize columns, chunked in
+// folded pairs); with more than one partition their digests are merged with merge_many.
+__global__ PG_KERNEL void hash_rows_kernel(const fe* __restrict__ M, uint32_t ncols, size_t nrows,
                                                         uint32_t psize, fe* __restrict__ out) {
-  size_t row = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= nrows) return;
-  uint32_t c0 = blockIdx.y * psize;
-  uint32_t len = min(psize, ncols - c0);
-  const fe* base = M + (size_t)c0 * nrows + row;
-  fe d = sponge<DOM_ELEMS>((int)((len + 1) / 2), [&](int j) {
-    fe a = base[(size_t)(2 * j) * nrows];
-    fe b = (2u * j + 1 < len) ? base[(size_t)(2 * j + 1) * nrows] : fe_zero();
-    return fold_pair(a, b);
-  });
-  out[(size_t)blockIdx.y * nrows + row] = d;
+  PG_SETUP();
+  const bool live = P.g < PG_PER_WAVE && item < nrows;
+  const size_t row = live ? item : 0;
+  const uint32_t np = (ncols + psize - 1) / psize;
+  const bool merge = psize != ncols;  // partitioned rows end in merge_many, even of one digest
+  fe keep0 = fe_zero(), keep1 = fe_zero(), d = fe_zero();
+  for (uint32_t p = 0; p < np; p++) {
+    const uint32_t c0 = p * psize;
+    const uint32_t len = min(psize, ncols - c0);
+    const fe* base = M + (size_t)c0 * nrows + row;
+    d = pg_sponge<DOM_ELEMS>(P, live, (int)((len + 1) / 2), [&](int j) {
+      fe a = base[(size_t)(2 * j) * nrows];
+      fe b = (2u * j + 1 < len) ? base[(size_t)(2 * j + 1) * nrows] : fe_zero();
+      return fold_pair(a, b);
+    });
+    if (merge) {  // message p of merge_many is absorbed by lane (p+1) % 10 of block (p+1) / 10
+      fe v = pg_bcast(P, d, 0);
+      if ((int)((p + 1) % 10) == P.j) {
+        if (p + 1 < 10) keep0 = v; else keep1 = v;
+      }
+    }
+  }
+  if (merge) d = pg_sponge<DOM_MANY>(P, live, (int)np, [&](int i) { return i + 1 < 10 ? keep0 : keep1; });
+  if (live && P.j == 0) out[row] = d;
 }
 
-__global__ __launch_bounds__(256) void merge_parts_kernel(const fe* __restrict__ parts, uint32_t np, size_t nrows,
-                                                          fe* __restrict__ out) {
-  size_t row = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= nrows) return;
-  out[row] = sponge<DOM_MANY>((int)np, [&](int j) { return parts[(size_t)j * nrows + row]; });
+__global__ PG_KERNEL void merkle_level_kernel(fe* nodes, size_t lvl) {
+  PG_SETUP();
+  const bool live = P.g < PG_PER_WAVE && item < lvl;
+  const size_t i = lvl + (live ? item : 0);
+  fe d = pg_sponge<DOM_MERGE>(P, live, 2, [&](int j) { return nodes[2 * i + j]; });
+  if (live && P.j == 0) nodes[i] = d;
 }
 
-__global__ __launch_bounds__(256) void merkle_level_kernel(fe* nodes, size_t lvl) {
-  size_t i = lvl + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * lvl) return;
-  nodes[i] = merge2(nodes[2 * i], nodes[2 * i + 1]);
+__global__ PG_KERNEL void draw_kernel(fe seed, uint64_t base, size_t k, fe* out) {
+  PG_SETUP();
+  const bool live = P.g < PG_PER_WAVE && item < k;
+  const uint64_t ctr = base + 1 + item;
+  fe d = pg_sponge<DOM_INT>(P, live, 2, [&](int j) { return j == 0 ? seed : fe{ctr, 0}; });
+  if (live && P.j == 0) out[item] = d;
 }
 
-__global__ __launch_bounds__(256) void draw_kernel(fe seed, uint64_t base, size_t k, fe* out) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= k) return;
-  uint64_t ctr = base + 1 + i;
-  out[i] = sponge<DOM_INT>(2, [&](int j) { return j == 0 ? seed : fe{ctr, 0}; });
-}
-
-__global__ __launch_bounds__(256) void grind_kernel(fe seed, uint64_t base, uint32_t count, uint32_t bits,
+__global__ PG_KERNEL void grind_kernel(fe seed, uint64_t base, uint32_t count, uint32_t bits,
                                                     unsigned long long* best) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
-  uint64_t nonce = base + i;
-  fe h = sponge<DOM_INT>(2, [&](int j) { return j == 0 ? seed : fe{nonce, 0}; });
-  uint32_t tz = h.lo ? (uint32_t)__builtin_ctzll(h.lo) : 64u;
-  if (tz >= bits) atomicMin(best, (unsigned long long)nonce);
+  PG_SETUP();
+  const bool live = P.g < PG_PER_WAVE && item < count;
+  const uint64_t nonce = base + item;
+  fe h = pg_sponge<DOM_INT>(P, live, 2, [&](int j) { return j == 0 ? seed : fe{nonce, 0}; });
+  if (live && P.j == 0) {
+    uint32_t tz = h.lo ? (uint32_t)__builtin_ctzll(h.lo) : 64u;
+    if (tz >= bits) atomicMin(best, (unsigned long long)nonce);
+  }
 }
 
 void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np, uint32_t rate, fe* d_tmp, fe* d_out,
                       hipStream_t s) {
+  (void)d_tmp;
   uint32_t psize = ncols;
   if (np > 1) {
     psize = (ncols + np - 1) / np;
     if (psize < rate) psize = rate;  // PartitionOptions::partition_size, ExtensionDegree 1
   }
-  uint32_t nparts = (ncols + psize - 1) / psize;
-  dim3 blk(256), grid((unsigned)((nrows + 255) / 256), nparts);
-  if (psize == ncols) {
-    hash_rows_kernel<<<grid, blk, 0, s>>>(d_mat, ncols, nrows, psize, d_out);
-  } else {
-    hash_rows_kernel<<<grid, blk, 0, s>>>(d_mat, ncols, nrows, psize, d_tmp);
-    merge_parts_kernel<<<grid.x, blk, 0, s>>>(d_tmp, nparts, nrows, d_out);
-  }
+  hash_rows_kernel<<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, d_out);
 }
 
 void launch_merkle(fe* d_nodes, size_t n, hipStream_t s) {
-  for (size_t lvl = n / 2; lvl >= 1; lvl /= 2)
-    merkle_level_kernel<<<(unsigned)((lvl + 255) / 256), 256, 0, s>>>(d_nodes, lvl);
+  for (size_t lvl = n / 2; lvl >= 1; lvl /= 2) merkle_level_kernel<<<pg_blocks(lvl), 256, 0, s>>>(d_nodes, lvl);
 }
 
 void launch_draws(fe seed, uint64_t base, size_t k, fe* d_out, hipStream_t s) {
-  if (k) draw_kernel<<<(unsigned)((k + 255) / 256), 256, 0, s>>>(seed, base, k, d_out);
+  if (k) draw_kernel<<<pg_blocks(k), 256, 0, s>>>(seed, base, k, d_out);
 }
 
 void launch_grind(fe seed, uint64_t base, uint32_t count, uint32_t bits, unsigned long long* d_best, hipStream_t s) {
-  grind_kernel<<<(count + 255) / 256, 256, 0, s>>>(seed, base, count, bits, d_best);
+  grind_kernel<<<pg_blocks(count), 256, 0, s>>>(seed, base, count, bits, d_best);
 }
 
 // =====================================================================================
@@ -301,14 +381,14 @@ void launch_grind(fe seed, uint64_t base, uint32_t count, uint32_t bits, unsigne
 // A pass covers global half-sizes H in {S, 2S, .., 2^(r-1) S}.  Group q of 2^r elements:
 // L = q mod S, Hb = q / S, element t at Hb*S*2^r + t*S + L.  4096 elements per workgroup.
 // =====================================================================================
-constexpr int NTT_ELEMS = 4096;
+constexpr int NTT_ELEMS = 2048;  // per workgroup: 34 KB of LDS -> 4 workgroups (16 waves) per CU
 
 __device__ __forceinline__ uint32_t bitrev(uint32_t x, int logn) { return logn ? (__brev(x) >> (32 - logn)) : 0; }
 
 template <bool DIF>
 __global__ __launch_bounds__(256) void ntt_pass_kernel(fe* __restrict__ data, size_t ncols, int logN, int r,
                                                        int logS, const fe* __restrict__ roots, int logTab) {
-  __shared__ fe buf[NTT_ELEMS + 256];
+  __shared__ fe buf[NTT_ELEMS + NTT_ELEMS / 16];
   const int R = 1 << r;
   const int G = NTT_ELEMS >> r;
   const size_t S = (size_t)1 << logS;
@@ -334,28 +414,28 @@ __global__ __launch_bounds__(256) void ntt_pass_kernel(fe* __restrict__ data, si
   }
   __syncthreads();
   for (int st = 0; st < r; st++) {
-    int lh = DIF ? (r - 1 - st) : st;  // log2 of local half size
-    int h = 1 << lh;
+    const int lh = DIF ? (r - 1 - st) : st;  // log2 of local half size
+    const int h = 1 << lh;
+    const int shift = logTab - (lh + logS + 1);
     for (int u = threadIdx.x; u < NTT_ELEMS / 2; u += 256) {
-      int g = u >> (r - 1);
-      int w = u & ((R >> 1) - 1);
-      int k = w & (h - 1);
-      int t0 = ((w >> lh) << (lh + 1)) + k;
-      size_t qg = q0 + g;
-      size_t q = qg % groups_per_col;
-      size_t L = q & (S - 1);
-      // twiddle w_(2H)^((k*S + L)) with H = h*S  -> table index * Ntab/(2H)
-      size_t e = ((size_t)k << logS) + L;
-      int shift = logTab - (lh + logS + 1);
-      fe tw = roots[e << shift];
-      fe x0 = buf[g * pitch + t0], x1 = buf[g * pitch + t0 + h];
+      // groups vary fastest across lanes: consecutive lanes take consecutive L, so the
+      // twiddle loads w_(2H)^(k*S + L) are contiguous in the root table
+      const int g = u % G;
+      const int w = u / G;
+      const int k = w & (h - 1);
+      const int t0 = ((w >> lh) << (lh + 1)) + k;
+      const size_t q = (q0 + g) % groups_per_col;
+      const size_t L = q & (S - 1);
+      const fe tw = roots[(((size_t)k << logS) + L) << shift];
+      fe* p0 = &buf[g * pitch + t0];
+      const fe x0 = p0[0], x1 = p0[h];
       if (DIF) {
-        buf[g * pitch + t0] = fe_add(x0, x1);
-        buf[g * pitch + t0 + h] = fe_mul(fe_sub(x0, x1), tw);
+        p0[0] = fe_add(x0, x1);
+        p0[h] = fe_mul(fe_sub(x0, x1), tw);
       } else {
-        fe v = fe_mul(x1, tw);
-        buf[g * pitch + t0] = fe_add(x0, v);
-        buf[g * pitch + t0 + h] = fe_sub(x0, v);
+        const fe v = fe_mul(x1, tw);
+        p0[0] = fe_add(x0, v);
+        p0[h] = fe_sub(x0, v);
       }
     }
     __syncthreads();
@@ -755,15 +835,16 @@ void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Nt
 }
 
 // FRI layer leaves: hash_elements([e_i, e_{i+Nd/2}]) (FriProver::build_layer, folding 2)
-__global__ __launch_bounds__(256) void fri_leaf_kernel(const fe* ev, size_t half, fe* leaves) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= half) return;
-  fe m = fold_pair(ev[i], ev[i + half]);
-  leaves[i] = sponge<DOM_ELEMS>(1, [&](int) { return m; });
+__global__ PG_KERNEL void fri_leaf_kernel(const fe* ev, size_t half, fe* leaves) {
+  PG_SETUP();
+  const bool live = P.g < PG_PER_WAVE && item < half;
+  const size_t i = live ? item : 0;
+  fe d = pg_sponge<DOM_ELEMS>(P, live, 1, [&](int) { return fold_pair(ev[i], ev[i + half]); });
+  if (live && P.j == 0) leaves[i] = d;
 }
 void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s) {
   size_t h = Nd / 2;
-  fri_leaf_kernel<<<(unsigned)((h + 255) / 256), 256, 0, s>>>(d_ev, h, d_leaves);
+  fri_leaf_kernel<<<pg_blocks(h), 256, 0, s>>>(d_ev, h, d_leaves);
 }
 // fold: (v0+v1)/2 + alpha (v0-v1) / (2 x0), x0 = GENERATOR * g_d^i (constant offset, agg/trace.rs:764-800)
 __global__ void fri_fold_kernel(const fe* ev, size_t half, fe alpha, const fe* iroots, int shift, fe inv3, fe inv2,

@@ -83,9 +83,10 @@ def load_library():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"libzkl_hip.so not built ({LIB_PATH}); run `make -C zk-lisp_amd`")
-    lib = C.CDLL(LIB_PATH)
+    path = os.environ.get("ZKL_HIP_LIB", LIB_PATH)  # tools/: benchmark a variant build
+    if not os.path.exists(path):
+        raise ImportError(f"libzkl_hip.so not built ({path}); run `make -C zk-lisp_amd`")
+    lib = C.CDLL(path)
     P = C.POINTER
     lib.zkl_hip_init.argtypes = [C.c_int, P(C.c_void_p)]
     lib.zkl_hip_destroy.argtypes = [C.c_void_p]
