@@ -164,13 +164,11 @@ def main():
         ms_tot, launches = kacc["trace_hash_rows"]
         per_launch_ms = ms_tot / max(launches, 1)
         N = n * 16
-        parts = opts.num_partitions
-        ps = W if parts == 1 else max(-(-W // parts), opts.hash_rate)
-        npart = -(-W // ps)
-        alg_bytes = W * N * 16 + npart * N * 16  # LDE read once + partition digests written
+        # fused partitioned row hash: the 2^20 x 204 LDE is read once, one digest per row written
+        alg_bytes = W * N * 16 + N * 16
         achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
         pm = perm_model(n)
-        perms_per_launch = N * (pm["row_perms"] - (1 if parts > 1 else 0))
+        perms_per_launch = N * pm["row_perms"]  # fused: partitions + merge_many per row
         mads_per_s = perms_per_launch * MADS_PER_PERM / (per_launch_ms * 1e-3) / 1e9
         traffic = load_traffic("hash_rows_kernel")
         out = {

@@ -152,6 +152,12 @@ int zkl_hip_merkle_tree(zkl_ctx* ctx, const void* d_leaves, uint32_t n_leaves, v
 int zkl_hip_lde(zkl_ctx* ctx, const void* d_values, uint32_t n_cols, uint32_t n_rows,
                 uint32_t blowup, void* d_coeffs_out, void* d_lde_out);
 
+/* Raw in-place radix-2 NTT on n_cols contiguous device columns of length n (stage test
+ * entry point).  dif != 0: natural order in, bit-reversed out (Gentleman-Sande);
+ * dif == 0: bit-reversed in, natural out (Cooley-Tukey).  inverse selects w_n^-1; no 1/n
+ * scaling.  out[k] = sum_j in[j] * w^(j*k) in the respective orders. */
+int zkl_hip_ntt(zkl_ctx* ctx, void* d_data, uint32_t n_cols, uint32_t n, int dif, int inverse);
+
 /* ---- workload generator (host, not the measured path) -------------------- */
 /* Synthetic VM-only straight-line segment: 2^log_n rows, width 204
  * ({vm, rom} layout), ops cycling Const/Add/Mov/Mul over r0..r7 with splitmix64

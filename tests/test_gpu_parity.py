@@ -98,11 +98,12 @@ def test_stage_hash_rows_and_merkle(oracle, gpu_ctx):
         gpu_ctx.free(d)
 
 
-def test_stage_lde_matches_oracle(oracle, gpu_ctx):
-    """zkl_hip_lde: coefficients and coset LDE (GENERATOR * <w_{16n}>) vs direct evaluation."""
+@pytest.mark.parametrize("log_n,blow", [(6, 16), (6, 8), (6, 2), (5, 32), (9, 4)])
+def test_stage_lde_matches_oracle(oracle, gpu_ctx, log_n, blow):
+    """zkl_hip_lde: coefficients and coset LDE (GENERATOR * <w_{blow*n}>) vs direct evaluation."""
     rng = random.Random(9)
     P = oracle.P
-    ncols, n, blow = 3, 64, 16
+    ncols, n = 3, 1 << log_n
     N = n * blow
     vals = [rng.randrange(P) for _ in range(ncols * n)]
     raw = (C.c_uint8 * (16 * ncols * n)).from_buffer_copy(b"".join(v.to_bytes(16, "little") for v in vals))
@@ -113,11 +114,11 @@ def test_stage_lde_matches_oracle(oracle, gpu_ctx):
     gpu_ctx.lde(d_v, ncols, n, blow, d_c, d_l)
     coef = gpu_ctx.download(d_c, len(raw))
     lde = gpu_ctx.download(d_l, 16 * ncols * N)
-    g = oracle.root_of_unity(6)
-    w = oracle.root_of_unity(10)
+    g = oracle.root_of_unity(log_n)
+    w = oracle.root_of_unity(log_n + blow.bit_length() - 1)
     for c in range(ncols):
         cs = [int.from_bytes(coef[16 * (c * n + k):16 * (c * n + k + 1)], "little") for k in range(n)]
-        for r in (0, 5, 63):
+        for r in (0, 5, n - 1):
             x = pow(g, r, P)
             assert sum(cs[k] * pow(x, k, P) for k in range(n)) % P == vals[c * n + r]
         for i in (0, 1, 17, N - 1):
@@ -126,3 +127,49 @@ def test_stage_lde_matches_oracle(oracle, gpu_ctx):
             assert int.from_bytes(lde[16 * (c * N + i):16 * (c * N + i + 1)], "little") == want
     for d in (d_v, d_c, d_l):
         gpu_ctx.free(d)
+
+
+@pytest.mark.parametrize("log_n", [1, 3, 8, 9, 10, 12])
+def test_stage_ntt_dif_dit(oracle, gpu_ctx, log_n):
+    """zkl_hip_ntt: DIF (natural -> bit-reversed) and DIT (bit-reversed -> natural), forward
+    and inverse, against direct evaluation at sampled outputs; sizes below and at the
+    context's twiddle-table size (log_n 12 forces a table rebuild)."""
+    rng = random.Random(11 + log_n)
+    P = oracle.P
+    n, ncols = 1 << log_n, 2
+    w = oracle.root_of_unity(log_n)
+    wi = pow(w, P - 2, P)
+    vals = [rng.randrange(P) for _ in range(ncols * n)]
+    raw = (C.c_uint8 * (16 * ncols * n)).from_buffer_copy(b"".join(v.to_bytes(16, "little") for v in vals))
+    d = gpu_ctx.alloc(len(raw))
+
+    def br(k):
+        return int(format(k, f"0{log_n}b")[::-1], 2) if log_n else 0
+
+    def get(buf, c, i):
+        return int.from_bytes(buf[16 * (c * n + i):16 * (c * n + i + 1)], "little")
+
+    samples = sorted({0, 1, n // 2, n - 1, rng.randrange(n), rng.randrange(n)})
+    for inverse in (False, True):
+        root = wi if inverse else w
+        # DIF: natural in, out[bitrev(k)] = sum_j a_j root^(jk)
+        gpu_ctx.upload(d, raw, len(raw))
+        gpu_ctx.ntt(d, ncols, n, dif=True, inverse=inverse)
+        out = gpu_ctx.download(d, len(raw))
+        for c in range(ncols):
+            a = vals[c * n:(c + 1) * n]
+            for k in samples:
+                want = sum(a[j] * pow(root, j * k, P) for j in range(n)) % P
+                assert get(out, c, br(k)) == want, (inverse, c, k)
+        # DIT: bit-reversed in, natural out: feed a[bitrev(j)] at position j
+        perm = [vals[c * n + br(j)] for c in range(ncols) for j in range(n)]
+        praw = (C.c_uint8 * (16 * ncols * n)).from_buffer_copy(b"".join(v.to_bytes(16, "little") for v in perm))
+        gpu_ctx.upload(d, praw, len(praw))
+        gpu_ctx.ntt(d, ncols, n, dif=False, inverse=inverse)
+        out = gpu_ctx.download(d, len(raw))
+        for c in range(ncols):
+            a = vals[c * n:(c + 1) * n]
+            for k in samples:
+                want = sum(a[j] * pow(root, j * k, P) for j in range(n)) % P
+                assert get(out, c, k) == want, ("dit", inverse, c, k)
+    gpu_ctx.free(d)

@@ -59,6 +59,26 @@ int main() {
     redc(col, o);
     if (!fe_eq(from26(o), fe_mul(acc, Rinv))) { if (bad++ < 10) printf("mds mismatch it=%d\n", it); }
   }
+  // mul_tw (NTT twiddle product): random twiddles, plus the operands seen on device where
+  // the REDC result exceeds 2^128 (twiddle w_512^128)
+  {
+    fe g = root_of_unity(9);
+    std::vector<fe> ws = {fe_pow64(g, 128), fe_pow64(g, 384), fe_pow64(g, 1)};
+    for (int i = 0; i < 64; i++) ws.push_back(fe{rng(), rng() >> 1});
+    std::vector<fe> as = {fe{0x618373d3c785bcbdull, 0x46ca9081269b2944ull}, fe{0x2b3a64ac8a8a20c7ull, 0x4d817dfe6e9ca187ull},
+                          fe{0xda9b84022150b7b7ull, 0x6617b8dd37180ea2ull}, fe{0x2018d63f9d60e4ddull, 0x67958cd2ead8edc8ull},
+                          fe{0, 0}, fe{1, 0}, fe{P_LO - 1, P_HI}};
+    for (int i = 0; i < 20000; i++) as.push_back(fe{rng(), rng() >> 1});
+    for (const fe& w : ws) {
+      uint32_t l[5];
+      limbs26(fe_mul(w, R), l);
+      uint4 l4 = make_uint4(l[0], l[1], l[2], l[3]);
+      uint32_t l1 = l[4];
+      MontTab t{&l4, &l1};
+      for (const fe& a : as)
+        if (!fe_eq(mul_tw(a, t, 0), fe_mul(a, w))) { if (bad++ < 10) printf("mul_tw mismatch\n"); }
+    }
+  }
   printf(bad ? "FAIL %d\n" : "OK\n", bad);
   return bad != 0;
 }

@@ -22,39 +22,49 @@ __host__ __device__ inline fe fe_one() { return fe{1, 0}; }
 __host__ __device__ inline bool fe_is_zero(fe a) { return (a.lo | a.hi) == 0; }
 __host__ __device__ inline bool fe_eq(fe a, fe b) { return a.lo == b.lo && a.hi == b.hi; }
 
-// a + b mod p
+#ifdef FE_ADD_U128
 __host__ __device__ inline fe fe_add(fe a, fe b) {
-  uint64_t lo = a.lo + b.lo;
-  uint64_t c0 = lo < a.lo;
-  uint64_t t = a.hi + b.hi;
-  uint64_t c1 = t < a.hi;
-  uint64_t hi = t + c0;
-  c1 |= hi < t;
-  if (c1) {  // wrapped past 2^128: add 2^128 - p = C_RED
-    uint64_t l2 = lo + C_RED;
-    hi += l2 < lo;
-    return fe{l2, hi};
-  }
-  if (hi == P_HI && lo >= P_LO) {  // >= p
-    return fe{lo - P_LO, 0};
-  }
-  return fe{lo, hi};
+  typedef unsigned __int128 u128;
+  const u128 A = ((u128)a.hi << 64) | a.lo, B = ((u128)b.hi << 64) | b.lo;
+  const u128 P = ((u128)P_HI << 64) | P_LO;
+  const u128 s = A + B;
+  const bool carry = s < A;
+  const u128 t = s - P;
+  const u128 r = (carry || s >= P) ? t : s;
+  return fe{(uint64_t)r, (uint64_t)(r >> 64)};
+}
+__host__ __device__ inline fe fe_sub(fe a, fe b) {
+  typedef unsigned __int128 u128;
+  const u128 A = ((u128)a.hi << 64) | a.lo, B = ((u128)b.hi << 64) | b.lo;
+  const u128 P = ((u128)P_HI << 64) | P_LO;
+  const u128 d = A - B;
+  const u128 r = A < B ? d + P : d;
+  return fe{(uint64_t)r, (uint64_t)(r >> 64)};
+}
+#else
+// a + b mod p (inputs canonical), branch-free: with s = a + b mod 2^128, the result is
+// s + C (mod 2^128) exactly when a + b >= p, i.e. when either addition carries out.
+__host__ __device__ inline fe fe_add(fe a, fe b) {
+  unsigned long long c0, c1, d0, d1;
+  const unsigned long long lo = __builtin_addcll(a.lo, b.lo, 0, &c0);
+  const unsigned long long hi = __builtin_addcll(a.hi, b.hi, c0, &c1);
+  const unsigned long long tlo = __builtin_addcll(lo, C_RED, 0, &d0);
+  const unsigned long long thi = __builtin_addcll(hi, 0, d0, &d1);
+  return (c1 | d1) ? fe{tlo, thi} : fe{lo, hi};
 }
 
+// a - b mod p: on borrow the wrapped difference d needs + p = - C (mod 2^128)
 __host__ __device__ inline fe fe_sub(fe a, fe b) {
-  uint64_t lo = a.lo - b.lo;
-  uint64_t br0 = a.lo < b.lo;
-  uint64_t t = a.hi - b.hi;
-  uint64_t br1 = a.hi < b.hi;
-  uint64_t hi = t - br0;
-  br1 |= t < br0;
-  if (br1) {  // negative: add p == subtract C_RED modulo 2^128
-    uint64_t l2 = lo - C_RED;
-    hi -= lo < C_RED;
-    return fe{l2, hi};
-  }
-  return fe{lo, hi};
+  unsigned long long b0, b1, e0, e1;
+  const unsigned long long lo = __builtin_subcll(a.lo, b.lo, 0, &b0);
+  const unsigned long long hi = __builtin_subcll(a.hi, b.hi, b0, &b1);
+  const unsigned long long tlo = __builtin_subcll(lo, C_RED, 0, &e0);
+  const unsigned long long thi = __builtin_subcll(hi, 0, e0, &e1);
+  (void)e1;
+  return b1 ? fe{tlo, thi} : fe{lo, hi};
 }
+
+#endif
 
 __host__ __device__ inline fe fe_neg(fe a) { return fe_sub(fe_zero(), a); }
 

@@ -44,12 +44,24 @@ void launch_draws(fe seed, uint64_t base, size_t k, fe* d_out, hipStream_t s);
 void launch_grind(fe seed, uint64_t base, uint32_t count, uint32_t bits, unsigned long long* d_best, hipStream_t s);
 
 // ---- NTT ---------------------------------------------------------------------
+// Twiddle table in Montgomery/26-bit-limb form (entry = limbs of w * 2^156 mod p),
+// split into limbs 0..3 (l4) and limb 4 (l1); a twiddle product is then one REDC.
+struct MontTab {
+  const uint4* l4;
+  const uint32_t* l1;
+};
+// host: fill a device buffer of N*20 bytes (l4 then l1) from the canonical table w[0..N)
+void build_mont_table(const fe* h_w, size_t N, void* d_buf, hipStream_t s);
+inline MontTab mont_tab(const void* d_buf, size_t N) {
+  return MontTab{(const uint4*)d_buf, (const uint32_t*)((const char*)d_buf + N * 16)};
+}
 // In-place radix-2 stages on n_cols contiguous columns of length N (power of two).
 // dif=true : stages H = 2^hi_log .. 2^lo_log (descending), natural -> bit-reversed
 // dif=false: stages H = 2^lo_log .. 2^hi_log (ascending),  bit-reversed -> natural
-// roots: table of w_Ntab^e (e < Ntab), Ntab >= N; inverse tables give inverse transforms.
+// roots: stage-major Montgomery table (build_mont_table) of size Ntab >= N; tables built from
+// inverse roots give inverse transforms.
 void launch_ntt_stages(fe* d_data, size_t n_cols, size_t N, bool dif, int lo_log, int hi_log,
-                       const fe* d_roots, size_t Ntab, hipStream_t s);
+                       MontTab roots, size_t Ntab, hipStream_t s);
 // out[c*N + B*j + t] = in[c*stride + off + src(j)*estride] * scale[bitrev_n(j)] * mult for t < B (B = N/n);
 // src(j) = j or n-1-j
 void launch_broadcast(const fe* d_in, size_t in_col_stride, size_t in_elem_stride, size_t in_offset,

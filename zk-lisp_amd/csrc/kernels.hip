@@ -7,6 +7,8 @@
 // computing the same residues, independent of evaluation order.
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "kernels.h"
 
 namespace zkl {
@@ -385,24 +387,90 @@ constexpr int NTT_ELEMS = 2048;  // per workgroup: 34 KB of LDS -> 4 workgroups 
 
 __device__ __forceinline__ uint32_t bitrev(uint32_t x, int logn) { return logn ? (__brev(x) >> (32 - logn)) : 0; }
 
+// x * w for a twiddle w given as limbs of w*2^156 (MontTab): REDC(x * wR) = x*w, then one
+// conditional subtraction makes it canonical.
+__host__ __device__ __forceinline__ fe mul_tw(fe a, MontTab t, size_t e) {
+  const uint4 q = t.l4[e];
+  const uint32_t wm[5] = {q.x, q.y, q.z, q.w, t.l1[e]};
+  uint32_t l[5], o[5];
+  to26(a, l);
+  mont_mul(l, wm, o);
+  // the REDC result lies in (0, p + 2^100): bit 128 (limb 4, bit 24) may be set
+  typedef unsigned __int128 u128;
+  const u128 v = (u128)o[0] + ((u128)o[1] << 26) + ((u128)o[2] << 52) + ((u128)o[3] << 78) + ((u128)o[4] << 104);
+  const u128 P = ((u128)P_HI << 64) | P_LO;
+  const u128 r = (o[4] >> 24) ? v + C_RED : (v >= P ? v - P : v);  // v wrapped mod 2^128: Y - p = v + C
+#ifdef NTT_CHECK
+  {
+    uint64_t cc[10] = {wm[0], wm[1], wm[2], wm[3], wm[4], 0, 0, 0, 0, 0};
+    uint32_t wl[5];
+    redc(cc, wl);
+    u128 wv = (u128)wl[0] + ((u128)wl[1] << 26) + ((u128)wl[2] << 52) + ((u128)wl[3] << 78) + ((u128)wl[4] << 104);
+    if (wv >= P) wv -= P;
+    fe want = fe_mul(a, fe{(uint64_t)wv, (uint64_t)(wv >> 64)});
+    if (want.lo != (uint64_t)r || want.hi != (uint64_t)(r >> 64))
+      printf("mul_tw mismatch e=%lu a=%016lx%016lx got=%016lx%016lx want=%016lx%016lx o=%x %x %x %x %x\n", (unsigned long)e,
+             (unsigned long)a.hi, (unsigned long)a.lo, (unsigned long)(uint64_t)(r >> 64), (unsigned long)(uint64_t)r,
+             (unsigned long)want.hi, (unsigned long)want.lo, o[0], o[1], o[2], o[3], o[4]);
+  }
+#endif
+  return fe{(uint64_t)r, (uint64_t)(r >> 64)};
+}
+
+// Stage-major twiddle layout: entry H + j = w_(2H)^j for H = 1, 2, 4, .., N/2 and j < H, so
+// the twiddles of one radix-2 stage are contiguous (coalesced across consecutive L, and the
+// small stages of a pass share a few KB that stay in L2).  Valid for any NTT size <= N.
+void build_mont_table(const fe* w, size_t N, void* d_buf, hipStream_t s) {
+  const fe R = fe_pow64(fe{2, 0}, 156);
+  std::vector<uint32_t> l4(4 * N, 0), l1(N, 0);
+  for (size_t H = 1; H < N; H *= 2) {
+    const size_t step = N / (2 * H);
+    for (size_t j = 0; j < H; j++) {
+      uint32_t l[5];
+      limbs26(fe_mul(w[j * step], R), l);
+      for (int t = 0; t < 4; t++) l4[4 * (H + j) + t] = l[t];
+      l1[H + j] = l[4];
+    }
+  }
+  (void)hipMemcpyAsync(d_buf, l4.data(), N * 16, hipMemcpyHostToDevice, s);
+  (void)hipMemcpyAsync((char*)d_buf + N * 16, l1.data(), N * 4, hipMemcpyHostToDevice, s);
+  (void)hipStreamSynchronize(s);
+}
+
 template <bool DIF>
 __global__ __launch_bounds__(256) void ntt_pass_kernel(fe* __restrict__ data, size_t ncols, int logN, int r,
-                                                       int logS, const fe* __restrict__ roots, int logTab) {
+                                                       int logS, MontTab roots, int logTab) {
   __shared__ fe buf[NTT_ELEMS + NTT_ELEMS / 16];
   const int R = 1 << r;
   const int G = NTT_ELEMS >> r;
   const size_t S = (size_t)1 << logS;
-  const size_t groups_per_col = ((size_t)1 << logN) >> r;
-  const size_t total_groups = groups_per_col * ncols;
-  const size_t q0 = (size_t)blockIdx.x * G;
+  const int log_gpc = logN - r;  // groups per column = N / R
+  const size_t gpc = (size_t)1 << log_gpc;
   const bool gfast = S >= (size_t)G;
   const int pitch = R >= 16 ? R + 1 : R;  // pad: conflict-free 16-byte accesses
-
+  // Block -> groups.  When a column holds whole blocks, consecutive blocks walk the columns
+  // at a fixed group range, so concurrently running blocks share twiddles (same L) in L2.
+  size_t col_fixed = 0, qbase = 0;
+  const bool whole = gpc >= (size_t)G;
+  if (whole) {
+    col_fixed = blockIdx.x % (unsigned)ncols;
+    qbase = (size_t)(blockIdx.x / (unsigned)ncols) * G;
+  }
+  auto locate = [&](int g, size_t& col, size_t& q) -> bool {
+    if (whole) {
+      col = col_fixed;
+      q = qbase + g;
+      return true;
+    }
+    const size_t qg = (size_t)blockIdx.x * G + g;
+    col = qg >> log_gpc;
+    q = qg & (gpc - 1);
+    return col < ncols;
+  };
   auto addr = [&](int g, int t, bool& ok) -> size_t {
-    size_t qg = q0 + g;
-    ok = qg < total_groups;
-    size_t col = qg / groups_per_col, q = qg % groups_per_col;
-    size_t L = q & (S - 1), Hb = q >> logS;
+    size_t col, q;
+    ok = locate(g, col, q);
+    const size_t L = q & (S - 1), Hb = q >> logS;
     return (col << logN) + ((Hb << logS) << r) + (size_t)t * S + L;
   };
   for (int e = threadIdx.x; e < NTT_ELEMS; e += 256) {
@@ -416,26 +484,38 @@ __global__ __launch_bounds__(256) void ntt_pass_kernel(fe* __restrict__ data, si
   for (int st = 0; st < r; st++) {
     const int lh = DIF ? (r - 1 - st) : st;  // log2 of local half size
     const int h = 1 << lh;
-    const int shift = logTab - (lh + logS + 1);
-    for (int u = threadIdx.x; u < NTT_ELEMS / 2; u += 256) {
+    const size_t Hs = (size_t)h << logS;  // global half size: stage table base
+    // the four butterflies of a thread are disjoint: load all operands, then compute and store
+    constexpr int BPT = NTT_ELEMS / 2 / 256;
+    fe x0[BPT], x1[BPT];
+    size_t te[BPT];
+    int o0[BPT];
+#pragma unroll
+    for (int i = 0; i < BPT; i++) {
       // groups vary fastest across lanes: consecutive lanes take consecutive L, so the
       // twiddle loads w_(2H)^(k*S + L) are contiguous in the root table
+      const int u = threadIdx.x + 256 * i;
       const int g = u % G;
       const int w = u / G;
       const int k = w & (h - 1);
       const int t0 = ((w >> lh) << (lh + 1)) + k;
-      const size_t q = (q0 + g) % groups_per_col;
+      size_t colx, q;
+      locate(g, colx, q);
       const size_t L = q & (S - 1);
-      const fe tw = roots[(((size_t)k << logS) + L) << shift];
-      fe* p0 = &buf[g * pitch + t0];
-      const fe x0 = p0[0], x1 = p0[h];
+      te[i] = Hs + ((size_t)k << logS) + L;
+      o0[i] = g * pitch + t0;
+      x0[i] = buf[o0[i]];
+      x1[i] = buf[o0[i] + h];
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; i++) {
       if (DIF) {
-        p0[0] = fe_add(x0, x1);
-        p0[h] = fe_mul(fe_sub(x0, x1), tw);
+        buf[o0[i]] = fe_add(x0[i], x1[i]);
+        buf[o0[i] + h] = mul_tw(fe_sub(x0[i], x1[i]), roots, te[i]);
       } else {
-        const fe v = fe_mul(x1, tw);
-        p0[0] = fe_add(x0, v);
-        p0[h] = fe_sub(x0, v);
+        const fe v = mul_tw(x1[i], roots, te[i]);
+        buf[o0[i]] = fe_add(x0[i], v);
+        buf[o0[i] + h] = fe_sub(x0[i], v);
       }
     }
     __syncthreads();
@@ -451,7 +531,7 @@ __global__ __launch_bounds__(256) void ntt_pass_kernel(fe* __restrict__ data, si
 
 static int ilog2s(size_t n) { int k = 0; while (((size_t)1 << k) < n) k++; return k; }
 
-void launch_ntt_stages(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, const fe* roots, size_t Ntab,
+void launch_ntt_stages(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, MontTab roots, size_t Ntab,
                        hipStream_t s) {
   int logN = ilog2s(N), logTab = ilog2s(Ntab);
   if (hi < lo) return;

@@ -123,7 +123,7 @@ struct zkl_ctx {
   double stage_ms[ZKL_NUM_STAGES] = {0};
   // tables
   size_t tab_n = 0, tab_N = 0;
-  DBuf roots, iroots, opow, opow_n, pertab;
+  DBuf roots, iroots, mroots, miroots, opow, opow_n, pertab;
   // work buffers
   DBuf trace, coef, lde, parts, tree, ce, bvec, bm, clde, ctree, deep, draws, pw, oodv, asl, ast, asv, ars;
   DBuf fri_ev, fri_tree, best, gaddr, gout, flag;
@@ -208,6 +208,10 @@ void ensure_tables(zkl_ctx* C, size_t n, size_t N) {
     C->iroots.ensure(N * sizeof(fe));
     HIPCHECK(hipMemcpyAsync(C->roots.p, w.data(), N * sizeof(fe), hipMemcpyHostToDevice, s));
     HIPCHECK(hipMemcpyAsync(C->iroots.p, wi.data(), N * sizeof(fe), hipMemcpyHostToDevice, s));
+    C->mroots.ensure(N * 20);
+    C->miroots.ensure(N * 20);
+    build_mont_table(w.data(), N, C->mroots.p, s);
+    build_mont_table(wi.data(), N, C->miroots.p, s);
     HIPCHECK(hipStreamSynchronize(s));
     C->tab_N = N;
   }
@@ -283,6 +287,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   ensure_tables(C, n, N);
   const fe* roots = C->roots.f();
   const fe* iroots = C->iroots.f();
+  const MontTab mroots = mont_tab(C->mroots.p, C->tab_N), miroots = mont_tab(C->miroots.p, C->tab_N);
   const size_t Ntab = C->tab_N;
 
   StageTimer T(C);
@@ -300,9 +305,9 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
                           trace_on_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, s));
   {
     KScope k(C, KF_NTT);
-    launch_ntt_stages(C->coef.f(), W, n, true, 0, logn - 1, iroots, Ntab, s);  // -> n*coef, bit-reversed
+    launch_ntt_stages(C->coef.f(), W, n, true, 0, logn - 1, miroots, Ntab, s);  // -> n*coef, bit-reversed
     launch_broadcast(C->coef.f(), n, 1, 0, W, n, N, C->opow_n.f(), fe_one(), false, C->lde.f(), s);
-    launch_ntt_stages(C->lde.f(), W, N, false, ilog2(B), logN - 1, roots, Ntab, s);
+    launch_ntt_stages(C->lde.f(), W, N, false, ilog2(B), logN - 1, mroots, Ntab, s);
   }
   T.mark(1);
   // ---- trace commitment (commit_to_rows + MerkleTree)
@@ -366,9 +371,9 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   }
   {
     KScope k(C, KF_NTT);
-    launch_ntt_stages(C->bvec.f(), nb + 1, n, true, 0, logn - 1, roots, Ntab, s);  // forward, bit-reversed out
+    launch_ntt_stages(C->bvec.f(), nb + 1, n, true, 0, logn - 1, mroots, Ntab, s);  // forward, bit-reversed out
     launch_broadcast(C->bvec.f(), n, 1, 0, nb + 1, n, ce, C->opow.f(), fe_one(), true, C->bm.f(), s);
-    launch_ntt_stages(C->bm.f(), nb + 1, ce, false, ilog2(ce / n), logce - 1, roots, Ntab, s);
+    launch_ntt_stages(C->bm.f(), nb + 1, ce, false, ilog2(ce / n), logce - 1, mroots, Ntab, s);
   }
 
   // periodic table
@@ -409,7 +414,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   const fe inv3 = fe_inv(three), inv_ce = fe_inv(fe{ce, 0});
   {
     KScope k(C, KF_NTT);
-    launch_ntt_stages(C->ce.f(), 1, ce, true, 0, logce - 1, iroots, Ntab, s);  // ce * c_k * 3^k (bitrev)
+    launch_ntt_stages(C->ce.f(), 1, ce, true, 0, logce - 1, miroots, Ntab, s);  // ce * c_k * 3^k (bitrev)
     HIPCHECK(hipMemsetAsync(C->flag.p, 0, 4, s));
     launch_check_zero_range_bitrev(C->ce.f(), ce, (size_t)Cc * n, ce, (unsigned*)C->flag.p, s);
     for (int j = 0; j < Cc; j++) {
@@ -418,7 +423,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
       launch_broadcast(C->ce.f(), 0, ce / n, bitrev_u((uint32_t)j, loge), 1, n, N, nullptr, mult, false,
                        C->clde.f() + (size_t)j * N, s);
     }
-    launch_ntt_stages(C->clde.f(), Cc, N, false, ilog2(B), logN - 1, roots, Ntab, s);
+    launch_ntt_stages(C->clde.f(), Cc, N, false, ilog2(B), logN - 1, mroots, Ntab, s);
   }
   C->ctree.ensure(2 * N * sizeof(fe));
   {
@@ -847,6 +852,18 @@ int zkl_hip_merkle_tree(zkl_ctx* c, const void* d_leaves, uint32_t n, void* d_no
   });
 }
 
+int zkl_hip_ntt(zkl_ctx* c, void* d_data, uint32_t nc, uint32_t n, int dif, int inverse) {
+  if (!c || !d_data || n < 2 || (n & (n - 1))) return ZKL_E_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  return run_guarded(c, [&] {
+    HIPCHECK(hipSetDevice(c->device));
+    ensure_tables(c, c->tab_n ? c->tab_n : n, std::max<size_t>(n, c->tab_N));
+    const MontTab t = mont_tab(inverse ? c->miroots.p : c->mroots.p, c->tab_N);
+    launch_ntt_stages((fe*)d_data, nc, n, dif != 0, 0, ilog2(n) - 1, t, c->tab_N, c->stream);
+    HIPCHECK(hipStreamSynchronize(c->stream));
+  });
+}
+
 int zkl_hip_lde(zkl_ctx* c, const void* d_values, uint32_t nc, uint32_t n, uint32_t blowup, void* d_coeffs,
                 void* d_lde) {
   if (!c || n < 2 || (n & (n - 1)) || blowup < 1 || (blowup & (blowup - 1))) return ZKL_E_INVALID;
@@ -858,9 +875,9 @@ int zkl_hip_lde(zkl_ctx* c, const void* d_values, uint32_t nc, uint32_t n, uint3
     hipStream_t s = c->stream;
     fe* coef = (fe*)d_coeffs;
     HIPCHECK(hipMemcpyAsync(coef, d_values, (size_t)nc * n * sizeof(fe), hipMemcpyDeviceToDevice, s));
-    launch_ntt_stages(coef, nc, n, true, 0, ilog2(n) - 1, c->iroots.f(), c->tab_N, s);
+    launch_ntt_stages(coef, nc, n, true, 0, ilog2(n) - 1, mont_tab(c->miroots.p, c->tab_N), c->tab_N, s);
     launch_broadcast(coef, n, 1, 0, nc, n, N, c->opow_n.f(), fe_one(), false, (fe*)d_lde, s);
-    launch_ntt_stages((fe*)d_lde, nc, N, false, ilog2(blowup), ilog2(N) - 1, c->roots.f(), c->tab_N, s);
+    launch_ntt_stages((fe*)d_lde, nc, N, false, ilog2(blowup), ilog2(N) - 1, mont_tab(c->mroots.p, c->tab_N), c->tab_N, s);
     // return natural-order coefficients: scale n*c (bitrev) by 1/n and un-permute on host side is
     // not needed by callers; convert in place to natural order here
     std::vector<fe> h((size_t)nc * n), r((size_t)nc * n);

@@ -105,6 +105,7 @@ def load_library():
     lib.zkl_hip_synchronize.argtypes = [C.c_void_p]
     lib.zkl_select_partitions.argtypes = [C.c_uint32, C.c_uint32, P(C.c_uint32), P(C.c_uint32)]
     lib.zkl_synth_vm_segment.argtypes = [C.c_uint64, C.c_uint32, C.c_void_p, P(AirPublicInputs), P(C.c_uint32)]
+    lib.zkl_hip_ntt.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int]
     lib.zkl_hip_hash_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]
     lib.zkl_hip_merkle_tree.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
     lib.zkl_hip_lde.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]
@@ -248,6 +249,11 @@ class Context:
 
     def merkle_tree(self, d_leaves, n_leaves, d_nodes):
         rc = self.lib.zkl_hip_merkle_tree(self.ptr, C.c_void_p(d_leaves), n_leaves, C.c_void_p(d_nodes))
+        if rc:
+            self._err(rc)
+
+    def ntt(self, d_data, n_cols, n, dif=True, inverse=False):
+        rc = self.lib.zkl_hip_ntt(self.ptr, C.c_void_p(d_data), n_cols, n, int(dif), int(inverse))
         if rc:
             self._err(rc)
 
