@@ -10,7 +10,7 @@ queries, Proof::to_bytes) with the trace already resident in HBM.
 
 N > 1 is launched by torch.distributed.run, one rank per GPU; each rank proves its own
 segments (weak scaling, no data-path collective).  The barrier and the
-max-over-ranks timing use torch.distributed with the gloo backend on CPU tensors: the
+max-over-ranks timing (zkl_hip/dist.py) use torch.distributed's gloo backend: the
 prover's HIP runtime (/opt/rocm 7.2) owns the device, and loading torch's bundled ROCm
 runtime into the same process would create a second HIP runtime.
 Device synchronisation is zkl_hip_synchronize (hipDeviceSynchronize) on both sides.
@@ -109,14 +109,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
+    from zkl_hip import dist
+    rank, world, local_rank = dist.init()  # gloo control plane only (zkl_hip/dist.py)
 
     import zkl_hip
     ctx = zkl_hip.Context(local_rank)
@@ -133,12 +127,8 @@ def main():
     for _ in range(args.warmup):
         proof = ctx.prove_segment_device(d_trace, W, n, pi, opts)
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
     kacc = {}
-    barrier()
+    dist.barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -148,14 +138,9 @@ def main():
             a[0] += ms
             a[1] += cnt
     ctx.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
+    dist.barrier()
+    elapsed = dist.max_over_ranks(time.perf_counter() - t0)
     stages = ctx.stage_times()
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     if rank == 0:
         value = world * args.steps / elapsed
@@ -223,8 +208,7 @@ def main():
         print(json.dumps(out), flush=True)
     ctx.free(d_trace)
     ctx.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    dist.shutdown()
 
 
 if __name__ == "__main__":

@@ -3,10 +3,11 @@
  * the zk-lisp segment-proof hot path (zk-lisp-proof-winterfell + winterfell 0.13.1).
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
  *
- * Parity status: pinned by BLAKE3 spec vectors and the published
- * rollup-bench program commitment; the Poseidon/AIR/transcript layers follow the
- * reference sources cited per function; the Winterfell 0.13.1 byte/transcript conventions
- * (third-party, absent here) are a restatement from the published crate and are
+ * Parity status: BLAKE3 pinned by the spec vectors; f128 and Poseidon by
+ * an independent big-integer Python restatement (tests/pyref.py) and committed golden
+ * vectors; the AIR by trace satisfaction; the Poseidon/AIR/transcript layers follow the
+ * reference sources cited per function.  The Winterfell 0.13.1 byte/transcript conventions
+ * (third-party crate, absent here, no reference fixtures) are a restatement and are
  * "parity unpinned" against real Winterfell output.
  */
 #ifndef ORACLE_H

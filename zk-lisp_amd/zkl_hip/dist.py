@@ -1,0 +1,83 @@
+"""Multi-GPU coordination for segment proving.
+
+Segments are independent, so ranks (one process per GPU, launched by
+torch.distributed.run) prove disjoint segment sets with no data-path collective.  The
+only communication is control: a barrier around the timed region, the max-over-ranks
+elapsed time, and (for the aggregation hand-off) gathering step-proof bytes on rank 0.
+It runs on torch.distributed's gloo backend with CPU tensors: the prover owns the GPU
+through its own HIP runtime (runtime note)."""
+import os
+
+_dist = None
+
+
+def env():
+    """(rank, world_size, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init():
+    """Join the process group when world_size > 1 (gloo); returns (rank, world, local_rank)."""
+    global _dist
+    rank, world, local = env()
+    if world > 1 and _dist is None:
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            dist.init_process_group("gloo")
+        _dist = dist
+    return rank, world, local
+
+
+def segments_for_rank(n_segments, rank, world, rows=None):
+    """Segment ids proved by `rank`: greedy by rows (largest first onto the least-loaded
+    rank) when per-segment row counts are given, else round-robin i mod world."""
+    if rows is None:
+        return [i for i in range(n_segments) if i % world == rank]
+    load = [0] * world
+    owner = [0] * n_segments
+    for i in sorted(range(n_segments), key=lambda i: (-rows[i], i)):
+        r = min(range(world), key=lambda r: (load[r], r))
+        owner[i] = r
+        load[r] += rows[i]
+    return [i for i in range(n_segments) if owner[i] == rank]
+
+
+def barrier():
+    if _dist is not None:
+        _dist.barrier()
+
+
+def max_over_ranks(x):
+    if _dist is None:
+        return x
+    import torch
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    _dist.all_reduce(t, op=_dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x):
+    if _dist is None:
+        return x
+    import torch
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    _dist.all_reduce(t, op=_dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def gather_to_root(obj):
+    """Gather one picklable object per rank on rank 0 (list in rank order), None elsewhere."""
+    if _dist is None:
+        return [obj]
+    rank = _dist.get_rank()
+    out = [None] * _dist.get_world_size() if rank == 0 else None
+    _dist.gather_object(obj, out, dst=0)
+    return out
+
+
+def shutdown():
+    global _dist
+    if _dist is not None:
+        _dist.destroy_process_group()
+        _dist = None
