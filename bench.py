@@ -141,6 +141,7 @@ def main():
     dist.barrier()
     elapsed = dist.max_over_ranks(time.perf_counter() - t0)
     stages = ctx.stage_times()
+    host = ctx.host_times()
 
     if rank == 0:
         value = world * args.steps / elapsed
@@ -199,6 +200,7 @@ def main():
             "dominant_kernel_family": dom,
             "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kacc.items()},
             "stage_ms_last_step": {k: round(v, 3) for k, v in stages.items()},
+            "host_ms_last_step": {k: round(v, 3) for k, v in host.items()},
         }
         if world == 1 and not args.no_cpu_baseline:
             try:

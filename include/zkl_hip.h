@@ -115,6 +115,11 @@ int zkl_hip_prove_segment_device(zkl_ctx* ctx, const void* d_trace, uint32_t wid
                                  const zkl_air_public_inputs* pi, const zkl_proof_options* opts,
                                  uint8_t** proof_out, size_t* proof_len);
 
+/* Host-side wall times (ms) of the last proof on ctx: [0] host setup before the first
+ * kernel (AIR instance, assertions, uploads), [1] host time between the first and last
+ * stage marks not covered by device work, [2] the whole call.  Returns number written. */
+int zkl_hip_host_times(const zkl_ctx* ctx, double* out_ms, int max_n);
+
 /* Stage timings (ms) of the last proof on ctx; returns number written. */
 int zkl_hip_stage_times(const zkl_ctx* ctx, double* out_ms, int max_n);
 

@@ -66,6 +66,39 @@ __host__ __device__ inline fe fe_sub(fe a, fe b) {
 
 #endif
 
+// Branching forms: cheaper when operands are small (the constraint evaluator's selectors
+// and flags rarely wrap, so whole wavefronts skip the reduction).
+__host__ __device__ inline fe fe_add_sel(fe a, fe b) {
+  uint64_t lo = a.lo + b.lo;
+  uint64_t c0 = lo < a.lo;
+  uint64_t t = a.hi + b.hi;
+  uint64_t c1 = t < a.hi;
+  uint64_t hi = t + c0;
+  c1 |= hi < t;
+  if (c1) {  // wrapped past 2^128: add 2^128 - p = C_RED
+    uint64_t l2 = lo + C_RED;
+    hi += l2 < lo;
+    return fe{l2, hi};
+  }
+  if (hi == P_HI && lo >= P_LO) return fe{lo - P_LO, 0};
+  return fe{lo, hi};
+}
+
+__host__ __device__ inline fe fe_sub_sel(fe a, fe b) {
+  uint64_t lo = a.lo - b.lo;
+  uint64_t br0 = a.lo < b.lo;
+  uint64_t t = a.hi - b.hi;
+  uint64_t br1 = a.hi < b.hi;
+  uint64_t hi = t - br0;
+  br1 |= t < br0;
+  if (br1) {  // negative: add p == subtract C_RED modulo 2^128
+    uint64_t l2 = lo - C_RED;
+    hi -= lo < C_RED;
+    return fe{l2, hi};
+  }
+  return fe{lo, hi};
+}
+
 __host__ __device__ inline fe fe_neg(fe a) { return fe_sub(fe_zero(), a); }
 
 // ---------------------------------------------------------------- device multiply

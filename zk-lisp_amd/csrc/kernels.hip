@@ -626,12 +626,12 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
   const fe xn_inv = c_ce.xn_inv[i % blow];
   fe p_map = per[0], p_final = per[28], p_pad = per[29], p_pad_last = per[30];
   // p_last = L_{n-1}(x) = g^(n-1)/n * (x^n - 1) / (x - g^(n-1))
-  fe x_gl = fe_sub(x, c_ce.gl);
+  fe x_gl = fe_sub_sel(x, c_ce.gl);
   fe xn_m1 = c_ce.xn_m1[i % blow];
   fe p_last = fe_mul(fe_mul(c_ce.lagr, xn_m1), fe_inv(x_gl));
   fe s_low = fe_mul(p_last, p_map);
-  fe g_carry = fe_add(p_map, fe_sub(p_pad, p_pad_last));
-  for (int j = 0; j < 26; j++) g_carry = fe_add(g_carry, per[1 + j]);
+  fe g_carry = fe_add_sel(p_map, fe_sub_sel(p_pad, p_pad_last));
+  for (int j = 0; j < 26; j++) g_carry = fe_add_sel(g_carry, per[1 + j]);
   const fe rom_on = c_air.commit_nonzero ? fe_one() : fe_zero();
   const uint32_t m = c_air.vm_usage_mask;
 
@@ -648,56 +648,56 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
     fe sum_d0 = fe_zero(), sum_a = fe_zero(), sum_b = fe_zero(), sum_c = fe_zero(), sum_d1 = fe_zero();
     for (int r = 0; r < 8; r++) {
       fe v[5] = {cur(C.sel_dst0 + r), cur(C.sel_a + r), cur(C.sel_b + r), cur(C.sel_c + r), cur(C.sel_dst1 + r)};
-      sum_d0 = fe_add(sum_d0, v[0]); sum_a = fe_add(sum_a, v[1]); sum_b = fe_add(sum_b, v[2]);
-      sum_c = fe_add(sum_c, v[3]); sum_d1 = fe_add(sum_d1, v[4]);
+      sum_d0 = fe_add_sel(sum_d0, v[0]); sum_a = fe_add_sel(sum_a, v[1]); sum_b = fe_add_sel(sum_b, v[2]);
+      sum_c = fe_add_sel(sum_c, v[3]); sum_d1 = fe_add_sel(sum_d1, v[4]);
 #pragma unroll
-      for (int t = 0; t < 5; t++) A.emit(fe_add(fe_mul(p_map, fe_mul(v[t], fe_sub(v[t], one))), s_high));
+      for (int t = 0; t < 5; t++) A.emit(fe_add_sel(fe_mul(p_map, fe_mul(v[t], fe_sub_sel(v[t], one))), s_high));
     }
     fe bo[17];
 #pragma unroll
     for (int k = 0; k < 17; k++) bo[k] = cur(C.op[k]);
     enum { CONST, MOV, ADD, SUB, MUL, NEG, EQ, SEL, SPONGE, ASSERT, ABIT, ARANGE, DIVMOD, DIV128, MULWIDE, LOAD, STORE };
-    fe uses_a = fe_add(fe_add(fe_add(bo[MOV], bo[ADD]), fe_add(bo[SUB], bo[MUL])), fe_add(fe_add(bo[NEG], bo[EQ]), bo[SEL]));
-    uses_a = fe_add(uses_a, fe_add(fe_add(bo[DIVMOD], bo[DIV128]), fe_add(fe_add(bo[MULWIDE], bo[LOAD]), bo[STORE])));
-    fe uses_b = fe_add(fe_add(fe_add(bo[ADD], bo[SUB]), fe_add(bo[MUL], bo[EQ])), fe_add(bo[SEL], bo[DIVMOD]));
-    uses_b = fe_add(uses_b, fe_add(fe_add(bo[DIV128], bo[MULWIDE]), bo[STORE]));
-    fe uses_c = fe_add(fe_add(bo[SEL], bo[ASSERT]), fe_add(bo[ABIT], bo[ARANGE]));
+    fe uses_a = fe_add_sel(fe_add_sel(fe_add_sel(bo[MOV], bo[ADD]), fe_add_sel(bo[SUB], bo[MUL])), fe_add_sel(fe_add_sel(bo[NEG], bo[EQ]), bo[SEL]));
+    uses_a = fe_add_sel(uses_a, fe_add_sel(fe_add_sel(bo[DIVMOD], bo[DIV128]), fe_add_sel(fe_add_sel(bo[MULWIDE], bo[LOAD]), bo[STORE])));
+    fe uses_b = fe_add_sel(fe_add_sel(fe_add_sel(bo[ADD], bo[SUB]), fe_add_sel(bo[MUL], bo[EQ])), fe_add_sel(bo[SEL], bo[DIVMOD]));
+    uses_b = fe_add_sel(uses_b, fe_add_sel(fe_add_sel(bo[DIV128], bo[MULWIDE]), bo[STORE]));
+    fe uses_c = fe_add_sel(fe_add_sel(bo[SEL], bo[ASSERT]), fe_add_sel(bo[ABIT], bo[ARANGE]));
     fe op_any = fe_zero();
 #pragma unroll
-    for (int k = 0; k <= MULWIDE; k++) op_any = fe_add(op_any, bo[k]);
-    fe uses_d0 = fe_add(fe_sub(op_any, bo[SPONGE]), bo[LOAD]);
-    fe uses_d1 = fe_add(fe_add(bo[DIVMOD], bo[DIV128]), bo[MULWIDE]);
-    A.emit(fe_add(fe_mul(p_map, fe_sub(sum_d0, uses_d0)), s_low));
-    A.emit(fe_add(fe_mul(p_map, fe_sub(sum_a, uses_a)), s_low));
-    A.emit(fe_add(fe_mul(p_map, fe_sub(sum_b, uses_b)), s_low));
-    A.emit(fe_add(fe_mul(p_map, fe_sub(sum_c, uses_c)), s_low));
-    A.emit(fe_add(fe_mul(p_map, fe_sub(sum_d1, uses_d1)), s_low));
+    for (int k = 0; k <= MULWIDE; k++) op_any = fe_add_sel(op_any, bo[k]);
+    fe uses_d0 = fe_add_sel(fe_sub_sel(op_any, bo[SPONGE]), bo[LOAD]);
+    fe uses_d1 = fe_add_sel(fe_add_sel(bo[DIVMOD], bo[DIV128]), bo[MULWIDE]);
+    A.emit(fe_add_sel(fe_mul(p_map, fe_sub_sel(sum_d0, uses_d0)), s_low));
+    A.emit(fe_add_sel(fe_mul(p_map, fe_sub_sel(sum_a, uses_a)), s_low));
+    A.emit(fe_add_sel(fe_mul(p_map, fe_sub_sel(sum_b, uses_b)), s_low));
+    A.emit(fe_add_sel(fe_mul(p_map, fe_sub_sel(sum_c, uses_c)), s_low));
+    A.emit(fe_add_sel(fe_mul(p_map, fe_sub_sel(sum_d1, uses_d1)), s_low));
     for (int r = 0; r < 8; r++)
-      A.emit(fe_add(fe_mul(p_map, fe_mul(cur(C.sel_dst0 + r), cur(C.sel_dst1 + r))), s_high));
+      A.emit(fe_add_sel(fe_mul(p_map, fe_mul(cur(C.sel_dst0 + r), cur(C.sel_dst1 + r))), s_high));
     if (c_air.sponge_block) {
       for (int lane = 0; lane < 10; lane++) {
         for (int bit = 0; bit < 3; bit++) {
           fe v = cur(C.sel_s_bits + lane * 3 + bit);
-          A.emit(fe_add(fe_mul(p_map, fe_mul(v, fe_sub(v, one))), s_high));
+          A.emit(fe_add_sel(fe_mul(p_map, fe_mul(v, fe_sub_sel(v, one))), s_high));
         }
         fe a = cur(C.sel_s_active + lane);
-        A.emit(fe_add(fe_mul(p_map, fe_mul(a, fe_sub(a, one))), s_high));
+        A.emit(fe_add_sel(fe_mul(p_map, fe_mul(a, fe_sub_sel(a, one))), s_high));
       }
     }
     A.emit(s_high);
     fe op_sum = fe_zero();
 #pragma unroll
     for (int k = 0; k < 17; k++) {
-      A.emit(fe_add(fe_mul(p_map, fe_mul(bo[k], fe_sub(bo[k], one))), s_high));
-      op_sum = fe_add(op_sum, bo[k]);
+      A.emit(fe_add_sel(fe_mul(p_map, fe_mul(bo[k], fe_sub_sel(bo[k], one))), s_high));
+      op_sum = fe_add_sel(op_sum, bo[k]);
     }
-    A.emit(fe_add(fe_mul(p_map, fe_mul(op_sum, fe_sub(op_sum, one))), s_high));
+    A.emit(fe_add_sel(fe_mul(p_map, fe_mul(op_sum, fe_sub_sel(op_sum, one))), s_high));
 #pragma unroll
     for (int k = 0; k < 17; k++)
-      A.emit(fe_add(fe_mul(rom_on, fe_mul(p_map, fe_sub(bo[k], cur(C.rom_op_start + k)))), s_high));
+      A.emit(fe_add_sel(fe_mul(rom_on, fe_mul(p_map, fe_sub_sel(bo[k], cur(C.rom_op_start + k)))), s_high));
     fe pc_c = cur(C.pc), pc_n = nxt(C.pc);
-    A.emit(fe_add(fe_mul(rom_on, fe_mul(g_carry, fe_sub(pc_n, pc_c))), s_low));
-    A.emit(fe_add(fe_mul(rom_on, fe_mul(p_pad_last, fe_sub(pc_n, fe_add(pc_c, one)))), s_low));
+    A.emit(fe_add_sel(fe_mul(rom_on, fe_mul(g_carry, fe_sub_sel(pc_n, pc_c))), s_low));
+    A.emit(fe_add_sel(fe_mul(rom_on, fe_mul(p_pad_last, fe_sub_sel(pc_n, fe_add_sel(pc_c, one)))), s_low));
 
     // ---------------- VmAluAir (alu.rs:108-354)
     const bool use_eq = m & (1u << 6), use_divmod = m & (1u << 3), use_mulwide = m & (1u << 4),
@@ -707,77 +707,77 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
     fe a_val = fe_zero(), b_val = fe_zero(), c_val = fe_zero(), d0n = fe_zero(), d0c = fe_zero(), d1n = fe_zero();
     for (int r = 0; r < 8; r++) {
       fe rc = cur(C.r_start + r), rn = nxt(C.r_start + r);
-      a_val = fe_add(a_val, fe_mul(cur(C.sel_a + r), rc));
-      b_val = fe_add(b_val, fe_mul(cur(C.sel_b + r), rc));
-      c_val = fe_add(c_val, fe_mul(cur(C.sel_c + r), rc));
+      a_val = fe_add_sel(a_val, fe_mul(cur(C.sel_a + r), rc));
+      b_val = fe_add_sel(b_val, fe_mul(cur(C.sel_b + r), rc));
+      c_val = fe_add_sel(c_val, fe_mul(cur(C.sel_c + r), rc));
       fe sd0 = cur(C.sel_dst0 + r);
-      d0n = fe_add(d0n, fe_mul(sd0, rn));
-      d0c = fe_add(d0c, fe_mul(sd0, rc));
-      d1n = fe_add(d1n, fe_mul(cur(C.sel_dst1 + r), rn));
+      d0n = fe_add_sel(d0n, fe_mul(sd0, rn));
+      d0c = fe_add_sel(d0c, fe_mul(sd0, rc));
+      d1n = fe_add_sel(d1n, fe_mul(cur(C.sel_dst1 + r), rn));
     }
     for (int r = 0; r < 8; r++)
-      A.emit(fe_add(fe_mul(g_carry, fe_sub(nxt(C.r_start + r), cur(C.r_start + r))), s_low));
+      A.emit(fe_add_sel(fe_mul(g_carry, fe_sub_sel(nxt(C.r_start + r), cur(C.r_start + r))), s_low));
     fe imm = cur(C.imm);
     fe mode64 = cur(C.eq_inv);
     fe res = fe_mul(bo[CONST], imm);
-    res = fe_add(res, fe_mul(bo[MOV], a_val));
-    res = fe_add(res, fe_mul(bo[ADD], fe_add(a_val, b_val)));
-    res = fe_add(res, fe_mul(bo[SUB], fe_sub(a_val, b_val)));
-    res = fe_add(res, fe_mul(bo[MUL], fe_mul(a_val, b_val)));
-    res = fe_add(res, fe_mul(bo[NEG], fe_neg(a_val)));
-    res = fe_add(res, fe_mul(bo[SEL], fe_add(fe_mul(c_val, a_val), fe_mul(fe_sub(one, c_val), b_val))));
-    res = fe_add(res, fe_mul(bo[SPONGE], cur(C.lanes_start)));
-    if (use_eq) res = fe_add(res, fe_mul(bo[EQ], d0n));
-    if (use_assert) res = fe_add(res, bo[ASSERT]);
-    if (use_abit) res = fe_add(res, bo[ABIT]);
-    res = fe_add(res, fe_mul(bo[LOAD], imm));
+    res = fe_add_sel(res, fe_mul(bo[MOV], a_val));
+    res = fe_add_sel(res, fe_mul(bo[ADD], fe_add_sel(a_val, b_val)));
+    res = fe_add_sel(res, fe_mul(bo[SUB], fe_sub_sel(a_val, b_val)));
+    res = fe_add_sel(res, fe_mul(bo[MUL], fe_mul(a_val, b_val)));
+    res = fe_add_sel(res, fe_mul(bo[NEG], fe_neg(a_val)));
+    res = fe_add_sel(res, fe_mul(bo[SEL], fe_add_sel(fe_mul(c_val, a_val), fe_mul(fe_sub_sel(one, c_val), b_val))));
+    res = fe_add_sel(res, fe_mul(bo[SPONGE], cur(C.lanes_start)));
+    if (use_eq) res = fe_add_sel(res, fe_mul(bo[EQ], d0n));
+    if (use_assert) res = fe_add_sel(res, bo[ASSERT]);
+    if (use_abit) res = fe_add_sel(res, bo[ABIT]);
+    res = fe_add_sel(res, fe_mul(bo[LOAD], imm));
     fe bsum = fe_zero();
     if (use_arange) {
       fe pow2 = one;
-      for (int k = 0; k < 32; k++) { bsum = fe_add(bsum, fe_mul(pow2, cur(C.gadget_b + k))); pow2 = fe_add(pow2, pow2); }
-      res = fe_add(res, fe_mul(bo[ARANGE], fe_add(fe_mul(fe_sub(one, imm), bsum), imm)));
+      for (int k = 0; k < 32; k++) { bsum = fe_add_sel(bsum, fe_mul(pow2, cur(C.gadget_b + k))); pow2 = fe_add_sel(pow2, pow2); }
+      res = fe_add_sel(res, fe_mul(bo[ARANGE], fe_add_sel(fe_mul(fe_sub_sel(one, imm), bsum), imm)));
     }
     bool uses_two = use_divmod || use_mulwide || use_div128;
-    fe b_two = uses_two ? fe_add(fe_add(bo[DIVMOD], bo[MULWIDE]), bo[DIV128]) : fe_zero();
-    fe w0 = fe_add(fe_mul(fe_sub(one, b_two), res), fe_mul(b_two, d0n));
+    fe b_two = uses_two ? fe_add_sel(fe_add_sel(bo[DIVMOD], bo[MULWIDE]), bo[DIV128]) : fe_zero();
+    fe w0 = fe_add_sel(fe_mul(fe_sub_sel(one, b_two), res), fe_mul(b_two, d0n));
     fe w1 = fe_mul(b_two, d1n);
     for (int r = 0; r < 8; r++) {
       fe sd0 = cur(C.sel_dst0 + r), sd1 = cur(C.sel_dst1 + r);
-      fe keep = fe_sub(fe_sub(one, sd0), sd1);
-      fe rhs = fe_add(fe_add(fe_mul(keep, cur(C.r_start + r)), fe_mul(sd0, w0)), fe_mul(sd1, w1));
-      A.emit(fe_add(fe_mul(p_final, fe_sub(nxt(C.r_start + r), rhs)), s_write));
+      fe keep = fe_sub_sel(fe_sub_sel(one, sd0), sd1);
+      fe rhs = fe_add_sel(fe_add_sel(fe_mul(keep, cur(C.r_start + r)), fe_mul(sd0, w0)), fe_mul(sd1, w1));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_sub_sel(nxt(C.r_start + r), rhs)), s_write));
     }
-    fe diff = fe_sub(a_val, b_val);
+    fe diff = fe_sub_sel(a_val, b_val);
     fe inv = cur(C.eq_inv);
     if (use_eq) {
-      A.emit(fe_add(fe_mul(p_final, fe_mul(bo[EQ], fe_mul(d0n, diff))), s_eq));
-      A.emit(fe_add(fe_mul(p_final, fe_mul(bo[EQ], fe_sub(fe_sub(one, d0n), fe_mul(diff, inv)))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[EQ], fe_mul(d0n, diff))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[EQ], fe_sub_sel(fe_sub_sel(one, d0n), fe_mul(diff, inv)))), s_eq));
     }
     if (use_divmod) {
-      A.emit(fe_add(fe_mul(p_final, fe_mul(bo[DIVMOD], fe_sub(fe_sub(a_val, fe_mul(b_val, d0n)), d1n))), s_eq));
-      A.emit(fe_add(fe_mul(p_final, fe_mul(bo[DIVMOD], fe_sub(fe_mul(b_val, inv), one))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[DIVMOD], fe_sub_sel(fe_sub_sel(a_val, fe_mul(b_val, d0n)), d1n))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[DIVMOD], fe_sub_sel(fe_mul(b_val, inv), one))), s_eq));
     }
     const fe p264 = fe{0, 1};
     if (use_mulwide)
-      A.emit(fe_add(fe_mul(p_final, fe_mul(bo[MULWIDE], fe_sub(fe_mul(a_val, b_val), fe_add(d0n, fe_mul(d1n, p264))))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[MULWIDE], fe_sub_sel(fe_mul(a_val, b_val), fe_add_sel(d0n, fe_mul(d1n, p264))))), s_eq));
     if (use_div128) {
-      fe num128 = fe_add(fe_mul(a_val, p264), imm);
-      A.emit(fe_add(fe_mul(p_final, fe_mul(bo[DIV128], fe_sub(num128, fe_add(fe_mul(b_val, d0n), d1n)))), s_eq));
-      A.emit(fe_add(fe_mul(p_final, fe_mul(bo[DIV128], fe_sub(fe_mul(b_val, inv), one))), s_eq));
+      fe num128 = fe_add_sel(fe_mul(a_val, p264), imm);
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[DIV128], fe_sub_sel(num128, fe_add_sel(fe_mul(b_val, d0n), d1n)))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[DIV128], fe_sub_sel(fe_mul(b_val, inv), one))), s_eq));
     }
     if (use_assert)
-      A.emit(fe_add(fe_mul(p_final, fe_add(fe_mul(bo[ASSERT], fe_sub(c_val, one)), fe_mul(bo[SEL], fe_mul(c_val, fe_sub(c_val, one))))), s_eq));
-    if (use_abit) A.emit(fe_add(fe_mul(p_final, fe_mul(bo[ABIT], fe_mul(c_val, fe_sub(c_val, one)))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_add_sel(fe_mul(bo[ASSERT], fe_sub_sel(c_val, one)), fe_mul(bo[SEL], fe_mul(c_val, fe_sub_sel(c_val, one))))), s_eq));
+    if (use_abit) A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[ABIT], fe_mul(c_val, fe_sub_sel(c_val, one)))), s_eq));
     if (use_arange) {
       for (int k = 0; k < 32; k++) {
         fe bi = cur(C.gadget_b + k);
-        A.emit(fe_add(fe_mul(p_final, fe_mul(bo[ARANGE], fe_mul(bi, fe_sub(bi, one)))), s_eq));
+        A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[ARANGE], fe_mul(bi, fe_sub_sel(bi, one)))), s_eq));
       }
       const fe p232 = fe{1ull << 32, 0};
-      fe eq32 = fe_sub(c_val, bsum);
-      fe eq64 = fe_sub(c_val, fe_add(d0c, fe_mul(bsum, p232)));
-      fe eqt = fe_mul(imm, fe_add(fe_mul(mode64, eq64), fe_mul(fe_sub(one, mode64), eq32)));
-      A.emit(fe_add(fe_mul(p_final, fe_mul(bo[ARANGE], eqt)), s_eq));
+      fe eq32 = fe_sub_sel(c_val, bsum);
+      fe eq64 = fe_sub_sel(c_val, fe_add_sel(d0c, fe_mul(bsum, p232)));
+      fe eqt = fe_mul(imm, fe_add_sel(fe_mul(mode64, eq64), fe_mul(fe_sub_sel(one, mode64), eq32)));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[ARANGE], eqt)), s_eq));
     }
   }
   // ---------------- RomAir (rom.rs:57-120)
@@ -788,17 +788,17 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
     fe ms[3];
 #pragma unroll
     for (int k = 0; k < 3; k++)
-      ms[k] = fe_add(fe_add(fe_mul(c_air.rom_mds[k][0], s3[0]), fe_mul(c_air.rom_mds[k][1], s3[1])),
+      ms[k] = fe_add_sel(fe_add_sel(fe_mul(c_air.rom_mds[k][0], s3[0]), fe_mul(c_air.rom_mds[k][1], s3[1])),
                      fe_mul(c_air.rom_mds[k][2], s3[2]));
     fe sn[3] = {nxt(C.rom_s), nxt(C.rom_s + 1), nxt(C.rom_s + 2)};
     for (int j = 0; j < 27; j++) {
       fe gr = per[1 + j];
 #pragma unroll
-      for (int k = 0; k < 3; k++) A.emit(fe_mul(gr, fe_sub(sn[k], fe_add(ms[k], c_air.rom_rc[j][k]))));
+      for (int k = 0; k < 3; k++) A.emit(fe_mul(gr, fe_sub_sel(sn[k], fe_add_sel(ms[k], c_air.rom_rc[j][k]))));
     }
-    fe g_hold = fe_sub(p_pad, p_pad_last);
+    fe g_hold = fe_sub_sel(p_pad, p_pad_last);
 #pragma unroll
-    for (int k = 0; k < 3; k++) A.emit(fe_mul(g_hold, fe_sub(sn[k], cur(C.rom_s + k))));
+    for (int k = 0; k < 3; k++) A.emit(fe_mul(g_hold, fe_sub_sel(sn[k], cur(C.rom_s + k))));
     if (!fe_is_zero(p_map)) {
       uint32_t e0[9] = {0}, e1[9] = {0};
       int w = 0;
@@ -817,8 +817,8 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
           mul_acc(v, c_air.rom_w0[w], e0);
           mul_acc(v, c_air.rom_w1[w], e1);
         }
-      A.emit(fe_mul(p_map, fe_sub(cur(C.rom_s + 1), reduce288(e0))));
-      A.emit(fe_mul(p_map, fe_sub(cur(C.rom_s + 2), reduce288(e1))));
+      A.emit(fe_mul(p_map, fe_sub_sel(cur(C.rom_s + 1), reduce288(e0))));
+      A.emit(fe_mul(p_map, fe_sub_sel(cur(C.rom_s + 2), reduce288(e1))));
     } else {
       A.ix += 2;
     }
@@ -828,8 +828,8 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
   uint32_t bacc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint32_t nb = c_ce.n_bcols;
   for (uint32_t u = 0; u < nb; u++) mul_acc(cur((int)c_ce.bcol[u]), bm[(size_t)u * ce + i], bacc);
-  fe bsum2 = fe_sub(reduce288(bacc), bm[(size_t)nb * ce + i]);
-  fe v = fe_add(fe_mul(tsum, x_gl), bsum2);
+  fe bsum2 = fe_sub_sel(reduce288(bacc), bm[(size_t)nb * ce + i]);
+  fe v = fe_add_sel(fe_mul(tsum, x_gl), bsum2);
   out[i] = fe_mul(v, xn_inv);
 }
 

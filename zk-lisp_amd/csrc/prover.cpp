@@ -121,6 +121,7 @@ struct zkl_ctx {
   std::mutex mu;
   std::string err;
   double stage_ms[ZKL_NUM_STAGES] = {0};
+  double host_ms[3] = {0, 0, 0};  // host setup before the first kernel, host tail after the last, whole call
   // tables
   size_t tab_n = 0, tab_N = 0;
   DBuf roots, iroots, mroots, miroots, opow, opow_n, pertab;
@@ -263,6 +264,7 @@ __global__ void powers_kernel(fe base, fe mult, size_t n, int logn, fe* out) {
 
 void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t W, uint32_t n32,
                 const zkl_air_public_inputs& pi, const zkl_proof_options& o, std::vector<uint8_t>& out) {
+  const auto t_call0 = std::chrono::steady_clock::now();
   hipStream_t s = C->stream;
   const size_t n = n32;
   if (n < 32 || (n & (n - 1))) throw InvalidArg("trace length must be a power of two >= 32");
@@ -271,19 +273,14 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   if (o.batching_constraints != 0 || o.batching_deep != 0) throw InvalidArg("only BatchingMethod::Linear is supported");
   if (o.blowup_factor < 2 || (o.blowup_factor & (o.blowup_factor - 1))) throw InvalidArg("blowup must be a power of two");
   if (o.num_queries == 0 || o.num_queries > 255) throw InvalidArg("num_queries must be in 1..255");
-  AirInstance air;
-  std::string e = build_air(pi, W, n, air);
-  if (!e.empty()) throw InvalidArg(e);
-  if (o.blowup_factor < (uint32_t)air.ce_blowup) throw InvalidArg("blowup factor below constraint-evaluation blowup");
-  const size_t N = n * o.blowup_factor, ce = n * air.ce_blowup;
-  const int logn = ilog2(n), logN = ilog2(N), logce = ilog2(ce);
-  const int Cc = air.num_comp_cols;
+  const size_t N = n * o.blowup_factor;
+  const int logn = ilog2(n), logN = ilog2(N);
   const uint32_t B = o.blowup_factor;
   const fe g = root_of_unity(logn), three{3, 0};
   const Hasher& H = hasher();
+  if (W == 0 || W > 4096) throw InvalidArg("trace width must be in 1..4096");
 
   upload_hasher(s);
-  upload_air_consts(air.dev, s);
   ensure_tables(C, n, N);
   const fe* roots = C->roots.f();
   const fe* iroots = C->iroots.f();
@@ -292,6 +289,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
 
   StageTimer T(C);
   T.mark(0);
+  C->host_ms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call0).count();
   // ---- coin seed: Context::to_elements || AirPublicInputs::to_elements (agg/fs.rs:67-73)
   std::vector<fe> seed_el = context_elements(W, n, o);
   auto pie = pi_elements(pi);
@@ -322,6 +320,21 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     KScope k(C, KF_MERKLE);
     launch_merkle(C->tree.f(), N, s);
   }
+  // The AIR instance (layout, degrees, ~2.9e5 assertions at n = 2^16) is built on the host
+  // while the device runs the trace LDE and commitment queued above.
+  AirInstance air;
+  {
+    std::string e = build_air(pi, W, n, air);
+    if (e.empty() && o.blowup_factor < (uint32_t)air.ce_blowup) e = "blowup factor below constraint-evaluation blowup";
+    if (!e.empty()) {
+      (void)hipStreamSynchronize(s);
+      throw InvalidArg(e);
+    }
+  }
+  const size_t ce = n * air.ce_blowup;
+  const int logce = ilog2(ce);
+  const int Cc = air.num_comp_cols;
+  upload_air_consts(air.dev, s);
   fe troot;
   d2h(C, &troot, C->tree.f() + 1, sizeof(fe));
   coin.reseed(troot);
@@ -671,6 +684,12 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   T.finish();
   resolve_kernel_times(C);
   out.swap(P.v);
+  C->host_ms[2] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call0).count();
+  {
+    float gpu_ms = 0;
+    (void)hipEventElapsedTime(&gpu_ms, T.ev[0], T.ev[ZKL_NUM_STAGES]);
+    C->host_ms[1] = C->host_ms[2] - C->host_ms[0] - gpu_ms;  // host time not overlapped by the stream
+  }
 }
 
 int run_guarded(zkl_ctx* ctx, const std::function<void()>& f) {
@@ -759,6 +778,13 @@ int zkl_hip_prove_segment_device(zkl_ctx* c, const void* d_trace, uint32_t width
     prove_impl(c, d_trace, false, width, n, *pi, *o, v);
   });
   return rc ? rc : finish_proof(v, proof, len);
+}
+
+int zkl_hip_host_times(const zkl_ctx* c, double* out_ms, int max_n) {
+  if (!c || !out_ms) return ZKL_E_INVALID;
+  int k = std::min(max_n, 3);
+  for (int i = 0; i < k; i++) out_ms[i] = c->host_ms[i];
+  return k;
 }
 
 int zkl_hip_stage_times(const zkl_ctx* c, double* out, int max_n) {

@@ -97,6 +97,7 @@ def load_library():
                                           P(AirPublicInputs), P(ProofOptions), P(P(C.c_uint8)), P(C.c_size_t)]
     lib.zkl_hip_prove_segment_device.argtypes = lib.zkl_hip_prove_segment.argtypes
     lib.zkl_hip_stage_times.argtypes = [C.c_void_p, P(C.c_double), C.c_int]
+    lib.zkl_hip_host_times.argtypes = [C.c_void_p, P(C.c_double), C.c_int]
     lib.zkl_hip_kernel_times.argtypes = [C.c_void_p, P(C.c_double), P(C.c_int), C.c_int, P(C.c_char_p)]
     lib.zkl_hip_device_count.argtypes = [P(C.c_int)]
     lib.zkl_hip_device_alloc.argtypes = [C.c_void_p, C.c_size_t, P(C.c_void_p)]
@@ -200,6 +201,12 @@ class Context:
         arr = (C.c_double * len(STAGE_NAMES))()
         k = self.lib.zkl_hip_stage_times(self.ptr, arr, len(STAGE_NAMES))
         return dict(zip(STAGE_NAMES[:k], list(arr)[:k]))
+
+    def host_times(self):
+        """{setup, host_unoverlapped, call} wall ms of the last proof (host side)."""
+        arr = (C.c_double * 3)()
+        k = self.lib.zkl_hip_host_times(self.ptr, arr, 3)
+        return dict(zip(("setup", "host_unoverlapped", "call"), list(arr)[:k]))
 
     def kernel_times(self):
         """{family: (ms, launches)} of the last proof, from HIP events on the ctx stream."""
