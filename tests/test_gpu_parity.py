@@ -173,3 +173,34 @@ def test_stage_ntt_dif_dit(oracle, gpu_ctx, log_n):
                 want = sum(a[j] * pow(root, j * k, P) for j in range(n)) % P
                 assert get(out, c, k) == want, ("dit", inverse, c, k)
     gpu_ctx.free(d)
+
+
+def test_concurrent_contexts_same_device(gpu_ctx):
+    """Several contexts proving different segments at once on one device (threads; the
+    ctypes calls release the GIL) give the same bytes as one context proving them in turn:
+    per-proof constants are per context, not module-global."""
+    import threading
+    import zkl_hip
+    n = 1 << 9
+    jobs = []
+    for k in range(3):
+        t, pi, w = zkl_hip.synth_vm_segment(0x5EED0200 + k, 9)
+        opts = zkl_hip.proof_options(w, n, queries=16, grind=4)
+        jobs.append((t, pi, w, opts))
+    want = [gpu_ctx.prove_segment(t, w, n, pi, o) for t, pi, w, o in jobs]
+    ctxs = [zkl_hip.Context(0) for _ in jobs]
+    got = [None] * len(jobs)
+
+    def run(i):
+        t, pi, w, o = jobs[i]
+        for _ in range(3):
+            got[i] = ctxs[i].prove_segment(t, w, n, pi, o)
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(len(jobs))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    for c in ctxs:
+        c.close()
+    assert got == want

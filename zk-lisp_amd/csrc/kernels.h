@@ -26,16 +26,19 @@ struct HasherMont {
 };
 HasherMont make_hasher_mont(const HasherConsts& h);
 void upload_hasher_mont(const HasherMont& m, hipStream_t s);
-void upload_air_consts(const AirDevice& a, hipStream_t s);
-// transition composition coefficients alpha_j: copied device->constant from the draw buffer
-void upload_alphas_from_device(const fe* d_alphas, int n, hipStream_t s);
-void upload_deep_coeffs(const fe* h_coeffs, int n, hipStream_t s);
+struct CeParams;
+struct ProofConsts;  // per-proof constants in device memory, one block per context (below)
+void upload_air_consts(ProofConsts* dK, const AirDevice& a, hipStream_t s);
+// transition composition coefficients alpha_j: copied device->device from the draw buffer
+void upload_alphas_from_device(ProofConsts* dK, const fe* d_alphas, int n, hipStream_t s);
+void upload_deep_coeffs(ProofConsts* dK, const fe* h_coeffs, int n, hipStream_t s);
 
 // ---- hashing --------------------------------------------------------------
 // Row digests of a column-major matrix (ld = rows per column) with Winterfell partitioning.
 // d_tmp: scratch of n_parts * n_rows elements (unused when a single hash covers the row).
+// tag: 0 = trace commitment, 1 = composition commitment (distinct kernel symbols in profiles)
 void launch_hash_rows(const fe* d_mat, uint32_t n_cols, size_t n_rows, uint32_t num_partitions,
-                      uint32_t hash_rate, fe* d_tmp, fe* d_out, hipStream_t s);
+                      uint32_t hash_rate, fe* d_tmp, fe* d_out, hipStream_t s, int tag = 0);
 // Merkle tree: d_nodes[n..2n) must hold the leaves; fills d_nodes[1..n).
 void launch_merkle(fe* d_nodes, size_t n_leaves, hipStream_t s);
 // out[i] = merge_with_int(seed, base + 1 + i)   (RandomCoin::draw, counter base+1+i)
@@ -83,8 +86,17 @@ struct CeParams {
   uint32_t n_bcols;           // number of asserted columns in the boundary tables
   uint32_t bcol[64];          // their trace column indices
 };
+// Per-proof constants live in a per-context device block (not __constant__ symbols) so that
+// several contexts can prove concurrently on one device.
+struct ProofConsts {
+  AirDevice air;
+  CeParams ce;
+  fe alpha[512];  // transition composition coefficients
+  fe deep[512];   // DEEP coefficients (trace then composition columns)
+};
 void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab,
-                            const fe* d_bm /* (n_bcols + 1) x ce */, const CeParams& p, fe* d_out, hipStream_t s);
+                            const fe* d_bm /* (n_bcols + 1) x ce */, const CeParams& p, ProofConsts* dK, fe* d_out,
+                            hipStream_t s);
 // boundary vectors: vec[slot*n + step] = beta_a ; wv[s] = sum beta_a*value_a over assertions at step s
 void launch_boundary_scatter(const uint32_t* d_slot, const uint32_t* d_step, const fe* d_beta, size_t n_assert,
                              size_t n, fe* d_vecs, hipStream_t s);
@@ -101,8 +113,8 @@ struct DeepParams {
   uint32_t W, C;
   fe z, zg, sz, szg;
 };
-void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p, fe* d_out,
-                 hipStream_t s);
+void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p,
+                 const ProofConsts* dK, fe* d_out, hipStream_t s);
 void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s);
 void launch_fri_fold(const fe* d_ev, size_t Nd, fe alpha, const fe* d_iroots, size_t Ntab, fe* d_out, hipStream_t s);
 // gather 16-byte elements from absolute device addresses

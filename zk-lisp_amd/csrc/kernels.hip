@@ -14,22 +14,18 @@
 namespace zkl {
 
 __constant__ HasherConsts c_h;
-__constant__ AirDevice c_air;
-__constant__ fe c_alpha[512];
-__constant__ fe c_deep[512];
-__constant__ CeParams c_ce;
 
 void upload_hasher_consts(const HasherConsts& h, hipStream_t s) {
   (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_h), &h, sizeof h, 0, hipMemcpyHostToDevice, s);
 }
-void upload_air_consts(const AirDevice& a, hipStream_t s) {
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_air), &a, sizeof a, 0, hipMemcpyHostToDevice, s);
+void upload_air_consts(ProofConsts* dK, const AirDevice& a, hipStream_t s) {
+  (void)hipMemcpyAsync(&dK->air, &a, sizeof a, hipMemcpyHostToDevice, s);
 }
-void upload_alphas_from_device(const fe* d, int n, hipStream_t s) {
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_alpha), d, sizeof(fe) * n, 0, hipMemcpyDeviceToDevice, s);
+void upload_alphas_from_device(ProofConsts* dK, const fe* d, int n, hipStream_t s) {
+  (void)hipMemcpyAsync(dK->alpha, d, sizeof(fe) * n, hipMemcpyDeviceToDevice, s);
 }
-void upload_deep_coeffs(const fe* h, int n, hipStream_t s) {
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_deep), h, sizeof(fe) * n, 0, hipMemcpyHostToDevice, s);
+void upload_deep_coeffs(ProofConsts* dK, const fe* h, int n, hipStream_t s) {
+  (void)hipMemcpyAsync(dK->deep, h, sizeof(fe) * n, hipMemcpyHostToDevice, s);
 }
 
 // =====================================================================================
@@ -299,6 +295,8 @@ static inline unsigned pg_blocks(size_t items) {
 // ---- row hashing (Winterfell partitioned row hash): one group per row.  The row's
 // partitions are hashed one after another (hash_elements over psize columns, chunked in
 // folded pairs); with more than one partition their digests are merged with merge_many.
+// TAG only separates the trace (0) and composition (1) commitments in profiles
+template <int TAG>
 __global__ PG_KERNEL void hash_rows_kernel(const fe* __restrict__ M, uint32_t ncols, size_t nrows,
                                                         uint32_t psize, fe* __restrict__ out) {
   PG_SETUP();
@@ -356,14 +354,17 @@ __global__ PG_KERNEL void grind_kernel(fe seed, uint64_t base, uint32_t count, u
 }
 
 void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np, uint32_t rate, fe* d_tmp, fe* d_out,
-                      hipStream_t s) {
+                      hipStream_t s, int tag) {
   (void)d_tmp;
   uint32_t psize = ncols;
   if (np > 1) {
     psize = (ncols + np - 1) / np;
     if (psize < rate) psize = rate;  // PartitionOptions::partition_size, ExtensionDegree 1
   }
-  hash_rows_kernel<<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, d_out);
+  if (tag == 1)
+    hash_rows_kernel<1><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, d_out);
+  else
+    hash_rows_kernel<0><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, d_out);
 }
 
 void launch_merkle(fe* d_nodes, size_t n, hipStream_t s) {
@@ -605,12 +606,16 @@ void launch_geometric(fe base, const fe* roots, size_t step, size_t N, fe* out, 
 struct Acc {
   uint32_t a[9];
   int ix;
-  __device__ __forceinline__ void emit(fe v) { mul_acc(c_alpha[ix++], v, a); }
+  const fe* al;
+  __device__ __forceinline__ void emit(fe v) { mul_acc(al[ix++], v, a); }
 };
 
 __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restrict__ lde, const fe* __restrict__ roots,
                                                               int roots_shift, const fe* __restrict__ pertab,
-                                                              const fe* __restrict__ bm, fe* __restrict__ out) {
+                                                              const fe* __restrict__ bm,
+                                                              const ProofConsts* __restrict__ K, fe* __restrict__ out) {
+  const AirDevice& c_air = K->air;
+  const CeParams& c_ce = K->ce;
   const size_t ce = c_ce.ce, N = c_ce.N;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= ce) return;
@@ -639,6 +644,7 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
 #pragma unroll
   for (int k = 0; k < 9; k++) A.a[k] = 0;
   A.ix = 0;
+  A.al = K->alpha;
   const fe one = fe_one();
 
   if (c_air.feat_vm) {
@@ -834,10 +840,11 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
 }
 
 void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab, const fe* d_bm,
-                            const CeParams& p, fe* d_out, hipStream_t s) {
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_ce), &p, sizeof p, 0, hipMemcpyHostToDevice, s);
+                            const CeParams& p, ProofConsts* dK, fe* d_out, hipStream_t s) {
+  (void)hipMemcpyAsync(&dK->ce, &p, sizeof p, hipMemcpyHostToDevice, s);
   int shift = ilog2s(Ntab) - ilog2s(p.ce);
-  constraint_eval_kernel<<<(unsigned)((p.ce + 255) / 256), 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, d_out);
+  constraint_eval_kernel<<<(unsigned)((p.ce + 255) / 256), 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK,
+                                                                         d_out);
 }
 
 __global__ void boundary_scatter_kernel(const uint32_t* slot, const uint32_t* step, const fe* beta, size_t na, size_t n,
@@ -897,7 +904,9 @@ void launch_ood(const fe* d_coef, size_t ncols, size_t col_stride, size_t elem_s
 // DEEP composition over the LDE domain (agg/trace.rs:1126-1218 restates the formula):
 // sum_i g_i [(T_i(x)-T_i(z))/(x-z) + (T_i(x)-T_i(zg))/(x-zg)] + same for H_j
 __global__ __launch_bounds__(256) void deep_kernel(const fe* __restrict__ lde, const fe* __restrict__ clde,
-                                                   const fe* __restrict__ roots, int shift, DeepParams p, fe* out) {
+                                                   const fe* __restrict__ roots, int shift, DeepParams p,
+                                                   const ProofConsts* __restrict__ K, fe* out) {
+  const fe* c_deep = K->deep;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.N) return;
   uint32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -909,9 +918,10 @@ __global__ __launch_bounds__(256) void deep_kernel(const fe* __restrict__ lde, c
   fe num = fe_add(fe_mul(fe_sub(sv, p.sz), d2), fe_mul(fe_sub(sv, p.szg), d1));
   out[i] = fe_mul(num, fe_inv(fe_mul(d1, d2)));
 }
-void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p, fe* d_out,
-                 hipStream_t s) {
-  deep_kernel<<<(unsigned)((p.N + 255) / 256), 256, 0, s>>>(d_lde, d_clde, d_roots, ilog2s(Ntab) - ilog2s(p.N), p, d_out);
+void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p,
+                 const ProofConsts* dK, fe* d_out, hipStream_t s) {
+  deep_kernel<<<(unsigned)((p.N + 255) / 256), 256, 0, s>>>(d_lde, d_clde, d_roots, ilog2s(Ntab) - ilog2s(p.N), p, dK,
+                                                            d_out);
 }
 
 // FRI layer leaves: hash_elements([e_i, e_{i+Nd/2}]) (FriProver::build_layer, folding 2)

@@ -128,6 +128,7 @@ struct zkl_ctx {
   // work buffers
   DBuf trace, coef, lde, parts, tree, ce, bvec, bm, clde, ctree, deep, draws, pw, oodv, asl, ast, asv, ars;
   DBuf fri_ev, fri_tree, best, gaddr, gout, flag;
+  DBuf kconst;  // ProofConsts of the proof in flight on this context
   size_t pert_key_n = 0, pert_key_ce = 0;
   // kernel-family timers (HIP events on `stream` around each launch group)
   std::vector<hipEvent_t> evpool;
@@ -334,7 +335,9 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   const size_t ce = n * air.ce_blowup;
   const int logce = ilog2(ce);
   const int Cc = air.num_comp_cols;
-  upload_air_consts(air.dev, s);
+  C->kconst.ensure(sizeof(ProofConsts));
+  ProofConsts* dK = (ProofConsts*)C->kconst.p;
+  upload_air_consts(dK, air.dev, s);
   fe troot;
   d2h(C, &troot, C->tree.f() + 1, sizeof(fe));
   coin.reseed(troot);
@@ -349,7 +352,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     launch_draws(coin.seed, coin.counter, ndraw, C->draws.f(), s);
   }
   coin.counter += ndraw;
-  upload_alphas_from_device(C->draws.f(), air.n_tc, s);
+  upload_alphas_from_device(dK, C->draws.f(), air.n_tc, s);
 
   // boundary tables: per asserted column c, M_c = coset-LDE of
   // reverse(NTT_n(beta_c)); W likewise from sum_c beta*value.
@@ -416,7 +419,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->ce.ensure(ce * sizeof(fe));
   {
     KScope k(C, KF_CEVAL);
-    launch_constraint_eval(C->lde.f(), roots, Ntab, C->pertab.f(), C->bm.f(), cp, C->ce.f(), s);
+    launch_constraint_eval(C->lde.f(), roots, Ntab, C->pertab.f(), C->bm.f(), cp, dK, C->ce.f(), s);
   }
   T.mark(3);
 
@@ -441,7 +444,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->ctree.ensure(2 * N * sizeof(fe));
   {
     KScope k(C, KF_COMP_HASH);
-    launch_hash_rows(C->clde.f(), Cc, N, o.num_partitions, o.hash_rate, C->parts.f(), C->ctree.f() + N, s);
+    launch_hash_rows(C->clde.f(), Cc, N, o.num_partitions, o.hash_rate, C->parts.f(), C->ctree.f() + N, s, 1);
   }
   {
     KScope k(C, KF_MERKLE);
@@ -495,7 +498,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   launch_draws(coin.seed, coin.counter, W + Cc, C->draws.f(), s);
   coin.counter += W + Cc;
   d2h(C, gam.data(), C->draws.p, gam.size() * sizeof(fe));
-  upload_deep_coeffs(gam.data(), (int)gam.size(), s);
+  upload_deep_coeffs(dK, gam.data(), (int)gam.size(), s);
   DeepParams dp{};
   dp.N = N; dp.W = W; dp.C = Cc; dp.z = z; dp.zg = zg;
   dp.sz = fe_zero(); dp.szg = fe_zero();
@@ -504,7 +507,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->deep.ensure(N * sizeof(fe));
   {
     KScope k(C, KF_DEEP);
-    launch_deep(C->lde.f(), C->clde.f(), roots, Ntab, dp, C->deep.f(), s);
+    launch_deep(C->lde.f(), C->clde.f(), roots, Ntab, dp, dK, C->deep.f(), s);
   }
   T.mark(6);
 
