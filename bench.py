@@ -154,11 +154,20 @@ def main():
     ap.add_argument("--c3-inflight", type=str, default="1,2,4", help="contexts in flight to try for configs[2]")
     args = ap.parse_args()
 
+    # Only the result line goes to stdout: native libraries (gloo prints "[Gloo] Rank ..."
+    # from C++) write to fd 1, so fd 1 is pointed at stderr and the JSON line is written
+    # to a saved copy of the original stdout.
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
     from zkl_hip import dist
     rank, world, local_rank = dist.init()  # gloo control plane only (zkl_hip/dist.py)
 
     import zkl_hip
-    ctx = zkl_hip.Context(local_rank)
+    # ZKL_BENCH_DEVICE pins every rank to one device (rehearsing N > 1 on a 1-GPU box)
+    device = int(os.environ.get("ZKL_BENCH_DEVICE", local_rank))
+    ctx = zkl_hip.Context(device)
     log_n = args.log_n
     n = 1 << log_n
     trace, pi, W = zkl_hip.synth_vm_segment(0x5EED0001 + rank, log_n)
@@ -250,7 +259,7 @@ def main():
         if world == 1 and args.c3_segments > 0:
             c3 = {}
             for k in [int(x) for x in args.c3_inflight.split(",") if x]:
-                c3[str(k)] = round(c3_pipeline(zkl_hip, local_rank, log_n, args.c3_segments, k), 4)
+                c3[str(k)] = round(c3_pipeline(zkl_hip, device, log_n, args.c3_segments, k), 4)
             kbest = max(c3, key=lambda k: c3[k])
             out["c3_in_gpu_pipeline"] = {
                 "config": f"BASELINE configs[2] shape: {args.c3_segments} distinct synthetic 2^{log_n}-row segments on 1 GPU",
@@ -261,7 +270,7 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(args.cpu_sample_log_n, log_n)
             except Exception as e:  # reported, never fatal for the GPU number
                 out["cpu_baseline"] = {"value": None, "error": str(e)}
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=result_out, flush=True)
     ctx.free(d_trace)
     ctx.close()
     dist.shutdown()

@@ -116,7 +116,12 @@ struct DeepParams {
 void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p,
                  const ProofConsts* dK, fe* d_out, hipStream_t s);
 void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s);
-void launch_fri_fold(const fe* d_ev, size_t Nd, fe alpha, const fe* d_iroots, size_t Ntab, fe* d_out, hipStream_t s);
+// alpha read from device memory (written by launch_fri_coin)
+void launch_fri_fold(const fe* d_ev, size_t Nd, const fe* d_alpha, const fe* d_iroots, size_t Ntab, fe* d_out,
+                     hipStream_t s);
+// device transcript step of one FRI layer: coin[0] = merge(coin[0], *root); coin[1] = alpha
+// = merge_with_int(coin[0], 1); *root_out = *root
+void launch_fri_coin(fe* d_coin, const fe* d_root, fe* d_root_out, hipStream_t s);
 // gather 16-byte elements from absolute device addresses
 void launch_gather(const uint64_t* d_addrs, size_t k, fe* d_out, hipStream_t s);
 

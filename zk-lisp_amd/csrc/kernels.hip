@@ -371,6 +371,28 @@ void launch_merkle(fe* d_nodes, size_t n, hipStream_t s) {
   for (size_t lvl = n / 2; lvl >= 1; lvl /= 2) merkle_level_kernel<<<pg_blocks(lvl), 256, 0, s>>>(d_nodes, lvl);
 }
 
+// FRI transcript step on the device (DefaultRandomCoin: reseed with the layer root, then
+// draw alpha with counter 1): coin[0] = merge(coin[0], root); coin[1] = merge_with_int(
+// coin[0], 1); the root is also copied to *root_out.  One wave, group 0.
+__global__ __launch_bounds__(64) void fri_coin_kernel(fe* coin, const fe* root, fe* root_out) {
+  __shared__ __align__(16) uint32_t pg_lds[PG_WAVE_WORDS];
+  PGroup P;
+  pg_init(P, pg_lds);
+  const bool live = P.g == 0;
+  const fe seed = coin[0], r = *root;
+  fe s1 = pg_sponge<DOM_MERGE>(P, live, 2, [&](int j) { return j == 0 ? seed : r; });
+  s1 = pg_bcast(P, s1, 0);
+  fe a = pg_sponge<DOM_INT>(P, live, 2, [&](int j) { return j == 0 ? s1 : fe{1, 0}; });
+  if (threadIdx.x == 0) {
+    coin[0] = s1;
+    coin[1] = a;
+    *root_out = r;
+  }
+}
+void launch_fri_coin(fe* d_coin, const fe* d_root, fe* d_root_out, hipStream_t s) {
+  fri_coin_kernel<<<1, 64, 0, s>>>(d_coin, d_root, d_root_out);
+}
+
 void launch_draws(fe seed, uint64_t base, size_t k, fe* d_out, hipStream_t s) {
   if (k) draw_kernel<<<pg_blocks(k), 256, 0, s>>>(seed, base, k, d_out);
 }
@@ -937,19 +959,21 @@ void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s) {
   fri_leaf_kernel<<<pg_blocks(h), 256, 0, s>>>(d_ev, h, d_leaves);
 }
 // fold: (v0+v1)/2 + alpha (v0-v1) / (2 x0), x0 = GENERATOR * g_d^i (constant offset, agg/trace.rs:764-800)
-__global__ void fri_fold_kernel(const fe* ev, size_t half, fe alpha, const fe* iroots, int shift, fe inv3, fe inv2,
-                                fe* out) {
+__global__ void fri_fold_kernel(const fe* ev, size_t half, const fe* alpha_p, const fe* iroots, int shift, fe inv3,
+                                fe inv2, fe* out) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= half) return;
+  const fe alpha = *alpha_p;
   fe v0 = ev[i], v1 = ev[i + half];
   fe ix = fe_mul(inv3, iroots[i << shift]);
   out[i] = fe_mul(fe_add(fe_add(v0, v1), fe_mul(alpha, fe_mul(fe_sub(v0, v1), ix))), inv2);
 }
-void launch_fri_fold(const fe* d_ev, size_t Nd, fe alpha, const fe* d_iroots, size_t Ntab, fe* d_out, hipStream_t s) {
+void launch_fri_fold(const fe* d_ev, size_t Nd, const fe* d_alpha, const fe* d_iroots, size_t Ntab, fe* d_out,
+                     hipStream_t s) {
   size_t h = Nd / 2;
   fe inv3 = fe_inv(fe{3, 0}), inv2 = fe_inv(fe{2, 0});
-  fri_fold_kernel<<<(unsigned)((h + 255) / 256), 256, 0, s>>>(d_ev, h, alpha, d_iroots, ilog2s(Ntab) - ilog2s(Nd), inv3,
-                                                               inv2, d_out);
+  fri_fold_kernel<<<(unsigned)((h + 255) / 256), 256, 0, s>>>(d_ev, h, d_alpha, d_iroots, ilog2s(Ntab) - ilog2s(Nd),
+                                                               inv3, inv2, d_out);
 }
 
 __global__ void gather_kernel(const uint64_t* addrs, size_t k, fe* out) {

@@ -129,6 +129,7 @@ struct zkl_ctx {
   DBuf trace, coef, lde, parts, tree, ce, bvec, bm, clde, ctree, deep, draws, pw, oodv, asl, ast, asv, ars;
   DBuf fri_ev, fri_tree, best, gaddr, gout, flag;
   DBuf kconst;  // ProofConsts of the proof in flight on this context
+  DBuf fri_coin;  // device transcript of the FRI layers: seed, alpha, layer roots
   size_t pert_key_n = 0, pert_key_ce = 0;
   // kernel-family timers (HIP events on `stream` around each launch group)
   std::vector<hipEvent_t> evpool;
@@ -525,7 +526,12 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->fri_ev.ensure((ev_tot + 1) * sizeof(fe));
   C->fri_tree.ensure((tr_tot + 1) * sizeof(fe));
   auto layer_ev = [&](int d) -> fe* { return d == 0 ? C->deep.f() : C->fri_ev.f() + ev_off[d]; };
+  // the layer transcript (reseed with the layer root, draw alpha) runs on the device, so the
+  // whole layer chain is queued without a host round trip
   std::vector<fe> fri_roots(nl);
+  C->fri_coin.ensure((2 + (size_t)nl) * sizeof(fe));
+  fe* d_coin = C->fri_coin.f();
+  HIPCHECK(hipMemcpyAsync(d_coin, &coin.seed, sizeof(fe), hipMemcpyHostToDevice, s));
   for (int d = 0; d < nl; d++) {
     size_t Nd = N >> d, h = Nd / 2;
     fe* tr = C->fri_tree.f() + tr_off[d];
@@ -537,11 +543,16 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
       KScope k(C, KF_MERKLE);
       launch_merkle(tr, h, s);
     }
-    d2h(C, &fri_roots[d], tr + 1, sizeof(fe));
-    coin.reseed(fri_roots[d]);
-    fe alpha = coin.draw();
     KScope k(C, KF_FRI);
-    launch_fri_fold(layer_ev(d), Nd, alpha, iroots, Ntab, layer_ev(d + 1), s);
+    launch_fri_coin(d_coin, tr + 1, d_coin + 2 + d, s);
+    launch_fri_fold(layer_ev(d), Nd, d_coin + 1, iroots, Ntab, layer_ev(d + 1), s);
+  }
+  if (nl > 0) {
+    std::vector<fe> cs(2 + (size_t)nl);
+    d2h(C, cs.data(), d_coin, cs.size() * sizeof(fe));
+    for (int d = 0; d < nl; d++) fri_roots[d] = cs[2 + d];
+    coin.seed = cs[0];
+    coin.counter = 1;
   }
   size_t Nr = N >> nl;
   std::vector<fe> rem_ev(Nr);
