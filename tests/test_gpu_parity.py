@@ -60,8 +60,10 @@ def test_invalid_trace_rejected(gpu_ctx):
         gpu_ctx.prove_segment(t, w, 64, pi, opts)
 
 
-def test_full_size_deterministic(gpu_ctx):
-    """BASELINE config: 65536 rows, blowup 16, q 64, grind 16; two runs, same bytes."""
+def test_full_size_deterministic_and_verifies(oracle, gpu_ctx):
+    """BASELINE config: 65536 rows, blowup 16, q 64, grind 16; two runs give the same bytes
+    and the proof passes the oracle verifier (OOD identity, all Merkle openings, DEEP,
+    every FRI fold, remainder, proof of work)."""
     import zkl_hip
     n = 1 << 16
     t, pi, w = zkl_hip.synth_vm_segment(0x5EED0001, 16)
@@ -71,6 +73,13 @@ def test_full_size_deterministic(gpu_ctx):
     b = gpu_ctx.prove_segment(t, w, n, pi, opts)
     assert a == b
     print("full-size proof", len(a), hashlib.sha256(a).hexdigest(), gpu_ctx.stage_times())
+    oo = oracle.ProofOptions(*[getattr(opts, f) for f, _ in opts._fields_])
+    _, opi, _ = oracle.synth_segment(0x5EED0001, 16)
+    rc, err = oracle.verify(a, opi, oo)
+    assert rc == 0, err
+    bad = bytearray(a)
+    bad[len(a) // 2] ^= 4
+    assert oracle.verify(bytes(bad), opi, oo)[0] != 0
 
 
 def test_stage_hash_rows_and_merkle(oracle, gpu_ctx):
