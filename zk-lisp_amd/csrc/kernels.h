@@ -65,6 +65,12 @@ inline MontTab mont_tab(const void* d_buf, size_t N) {
 // inverse roots give inverse transforms.
 void launch_ntt_stages(fe* d_data, size_t n_cols, size_t N, bool dif, int lo_log, int hi_log,
                        MontTab roots, size_t Ntab, hipStream_t s);
+// Coset LDE evaluation: d_coef holds per column the bit-reversed coefficients already scaled
+// by the coset shift (c_k * 3^k at position bitrev(k)); d_out (N per column, natural order)
+// = evaluations over 3*<w_N>.  The first DIT pass reads the blowup copies straight from
+// d_coef.
+void launch_lde_from_coeffs(const fe* d_coef, size_t n_cols, size_t n, size_t N, MontTab roots, size_t Ntab, fe* d_out,
+                            hipStream_t s);
 // out[c*N + B*j + t] = in[c*stride + off + src(j)*estride] * scale[bitrev_n(j)] * mult for t < B (B = N/n);
 // src(j) = j or n-1-j
 void launch_broadcast(const fe* d_in, size_t in_col_stride, size_t in_elem_stride, size_t in_offset,

@@ -460,9 +460,13 @@ void build_mont_table(const fe* w, size_t N, void* d_buf, hipStream_t s) {
   (void)hipStreamSynchronize(s);
 }
 
+// src != nullptr (first DIT pass of an LDE): element i of column c is read from
+// src[c * (N >> src_logb) + (i >> src_logb)] instead of data, i.e. the blowup copies of the
+// (scaled, bit-reversed) coefficients are generated on load rather than materialised.
 template <bool DIF>
 __global__ __launch_bounds__(256) void ntt_pass_kernel(fe* __restrict__ data, size_t ncols, int logN, int r,
-                                                       int logS, MontTab roots, int logTab) {
+                                                       int logS, MontTab roots, int logTab, const fe* __restrict__ src,
+                                                       int src_logb) {
   __shared__ fe buf[NTT_ELEMS + NTT_ELEMS / 16];
   const int R = 1 << r;
   const int G = NTT_ELEMS >> r;
@@ -496,12 +500,15 @@ __global__ __launch_bounds__(256) void ntt_pass_kernel(fe* __restrict__ data, si
     const size_t L = q & (S - 1), Hb = q >> logS;
     return (col << logN) + ((Hb << logS) << r) + (size_t)t * S + L;
   };
+  const size_t Nmask = ((size_t)1 << logN) - 1;
   for (int e = threadIdx.x; e < NTT_ELEMS; e += 256) {
     int g = gfast ? (e % G) : (e >> r);
     int t = gfast ? (e / G) : (e & (R - 1));
     bool ok;
     size_t a = addr(g, t, ok);
-    buf[g * pitch + t] = ok ? data[a] : fe_zero();
+    fe v = fe_zero();
+    if (ok) v = src ? src[((a >> logN) << (logN - src_logb)) + ((a & Nmask) >> src_logb)] : data[a];
+    buf[g * pitch + t] = v;
   }
   __syncthreads();
   for (int st = 0; st < r; st++) {
@@ -554,8 +561,8 @@ __global__ __launch_bounds__(256) void ntt_pass_kernel(fe* __restrict__ data, si
 
 static int ilog2s(size_t n) { int k = 0; while (((size_t)1 << k) < n) k++; return k; }
 
-void launch_ntt_stages(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, MontTab roots, size_t Ntab,
-                       hipStream_t s) {
+static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, MontTab roots, size_t Ntab,
+                       const fe* src, int src_logb, hipStream_t s) {
   int logN = ilog2s(N), logTab = ilog2s(Ntab);
   if (hi < lo) return;
   if (dif) {
@@ -565,7 +572,8 @@ void launch_ntt_stages(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
       int logS = cur - r + 1;
       size_t groups = (N >> r) * ncols;
       size_t G = NTT_ELEMS >> r;
-      ntt_pass_kernel<true><<<(unsigned)((groups + G - 1) / G), 256, 0, s>>>(d, ncols, logN, r, logS, roots, logTab);
+      ntt_pass_kernel<true><<<(unsigned)((groups + G - 1) / G), 256, 0, s>>>(d, ncols, logN, r, logS, roots, logTab,
+                                                                             nullptr, 0);
       cur -= r;
     }
   } else {
@@ -574,10 +582,27 @@ void launch_ntt_stages(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
       int r = std::min(8, hi - cur + 1);
       size_t groups = (N >> r) * ncols;
       size_t G = NTT_ELEMS >> r;
-      ntt_pass_kernel<false><<<(unsigned)((groups + G - 1) / G), 256, 0, s>>>(d, ncols, logN, r, cur, roots, logTab);
+      ntt_pass_kernel<false><<<(unsigned)((groups + G - 1) / G), 256, 0, s>>>(d, ncols, logN, r, cur, roots, logTab,
+                                                                              cur == lo ? src : nullptr, src_logb);
       cur += r;
     }
   }
+}
+
+void launch_ntt_stages(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, MontTab roots, size_t Ntab,
+                       hipStream_t s) {
+  ntt_passes(d, ncols, N, dif, lo, hi, roots, Ntab, nullptr, 0, s);
+}
+
+void launch_lde_from_coeffs(const fe* d_coef, size_t ncols, size_t n, size_t N, MontTab roots, size_t Ntab, fe* d_out,
+                            hipStream_t s) {
+  const int logB = ilog2s(N / n);
+  if (logB == 0) {
+    (void)hipMemcpyAsync(d_out, d_coef, ncols * n * sizeof(fe), hipMemcpyDeviceToDevice, s);
+    ntt_passes(d_out, ncols, N, false, 0, ilog2s(N) - 1, roots, Ntab, nullptr, 0, s);
+    return;
+  }
+  ntt_passes(d_out, ncols, N, false, logB, ilog2s(N) - 1, roots, Ntab, d_coef, logB, s);
 }
 
 __global__ void broadcast_kernel(const fe* __restrict__ in, size_t in_col_stride, size_t in_elem_stride,

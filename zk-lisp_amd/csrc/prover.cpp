@@ -306,8 +306,8 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   {
     KScope k(C, KF_NTT);
     launch_ntt_stages(C->coef.f(), W, n, true, 0, logn - 1, miroots, Ntab, s);  // -> n*coef, bit-reversed
-    launch_broadcast(C->coef.f(), n, 1, 0, W, n, N, C->opow_n.f(), fe_one(), false, C->lde.f(), s);
-    launch_ntt_stages(C->lde.f(), W, N, false, ilog2(B), logN - 1, mroots, Ntab, s);
+    launch_scale_bitrev(C->coef.f(), W, n, C->opow_n.f(), s);                  // -> c_k * 3^k (coset shift)
+    launch_lde_from_coeffs(C->coef.f(), W, n, N, mroots, Ntab, C->lde.f(), s);
   }
   T.mark(1);
   // ---- trace commitment (commit_to_rows + MerkleTree)
@@ -463,16 +463,15 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   fe z = coin.draw(), zg = fe_mul(z, g);
   C->pw.ensure(4 * n * sizeof(fe));
   fe* pw = C->pw.f();
-  fe inv_n = fe_inv(fe{n, 0});
-  powers_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(z, inv_n, n, logn, pw);
-  powers_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(zg, inv_n, n, logn, pw + n);
+  // both the trace coefficients (c_k 3^k) and the composition columns carry the coset
+  // shift, so one pair of bit-reversed power vectors of z/3 and zg/3 serves both
   powers_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(fe_mul(z, inv3), fe_one(), n, logn, pw + 2 * n);
   powers_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(fe_mul(zg, inv3), fe_one(), n, logn, pw + 3 * n);
   C->oodv.ensure(2 * ((size_t)W + Cc) * sizeof(fe));
   fe* dood = C->oodv.f();
   {
     KScope k(C, KF_MISC);
-    launch_ood(C->coef.f(), W, n, 1, n, pw, pw + n, dood, dood + W, s);
+    launch_ood(C->coef.f(), W, n, 1, n, pw + 2 * n, pw + 3 * n, dood, dood + W, s);
     for (int j = 0; j < Cc; j++)
       launch_ood(C->ce.f() + bitrev_u((uint32_t)j, loge), 1, 0, ce / n, n, pw + 2 * n, pw + 3 * n,
                  dood + 2 * W + j, dood + 2 * W + Cc + j, s);
@@ -916,17 +915,24 @@ int zkl_hip_lde(zkl_ctx* c, const void* d_values, uint32_t nc, uint32_t n, uint3
     fe* coef = (fe*)d_coeffs;
     HIPCHECK(hipMemcpyAsync(coef, d_values, (size_t)nc * n * sizeof(fe), hipMemcpyDeviceToDevice, s));
     launch_ntt_stages(coef, nc, n, true, 0, ilog2(n) - 1, mont_tab(c->miroots.p, c->tab_N), c->tab_N, s);
-    launch_broadcast(coef, n, 1, 0, nc, n, N, c->opow_n.f(), fe_one(), false, (fe*)d_lde, s);
-    launch_ntt_stages((fe*)d_lde, nc, N, false, ilog2(blowup), ilog2(N) - 1, mont_tab(c->mroots.p, c->tab_N), c->tab_N, s);
+    launch_scale_bitrev(coef, nc, n, c->opow_n.f(), s);
+    launch_lde_from_coeffs(coef, nc, n, N, mont_tab(c->mroots.p, c->tab_N), c->tab_N, (fe*)d_lde, s);
     // return natural-order coefficients: scale n*c (bitrev) by 1/n and un-permute on host side is
     // not needed by callers; convert in place to natural order here
     std::vector<fe> h((size_t)nc * n), r((size_t)nc * n);
     HIPCHECK(hipMemcpyAsync(h.data(), coef, h.size() * sizeof(fe), hipMemcpyDeviceToHost, s));
     HIPCHECK(hipStreamSynchronize(s));
-    fe inv_n = fe_inv(fe{n, 0});
+    // coef[bitrev(k)] = c_k * 3^k
+    const fe inv3 = fe_inv(fe{3, 0});
     int logn = ilog2(n);
+    std::vector<fe> i3k(n);
+    i3k[0] = fe_one();
+    for (uint32_t k = 1; k < n; k++) i3k[k] = fe_mul(i3k[k - 1], inv3);
     for (uint32_t col = 0; col < nc; col++)
-      for (uint32_t j = 0; j < n; j++) r[(size_t)col * n + bitrev_u(j, logn)] = fe_mul(h[(size_t)col * n + j], inv_n);
+      for (uint32_t j = 0; j < n; j++) {
+        const uint32_t k = bitrev_u(j, logn);
+        r[(size_t)col * n + k] = fe_mul(h[(size_t)col * n + j], i3k[k]);
+      }
     HIPCHECK(hipMemcpyAsync(coef, r.data(), r.size() * sizeof(fe), hipMemcpyHostToDevice, s));
     HIPCHECK(hipStreamSynchronize(s));
   });
