@@ -6,6 +6,7 @@ zkl_hip_merkle_tree), for comparing kernel variants on the GPU box.
 
 Prints one JSON line: ms per call and Poseidon permutations/s for
   rows  : hash_rows over a 204-column x 2^log_rows matrix, 4 partitions (trace commitment)
+  ntt   : zkl_hip_ntt DIT over the same 204 columns (all log_rows stages)
   comp  : hash_rows over 7 columns, 4 partitions (composition commitment)
   tree  : full Merkle tree over 2^log_rows leaves
 Inputs are arbitrary field elements (< p); only timing is of interest here.
@@ -58,6 +59,10 @@ def main():
     ms = timeit(lambda: ctx.merkle_tree(d_out, n, d_nodes))
     out["tree_ms"] = round(ms, 3)
     out["tree_Mperm_s"] = round((n - 1) / ms / 1e3, 1)
+    # NTT: W columns of 2^log_rows, DIT (bit-reversed -> natural), all stages (3 passes at 2^20)
+    ms = timeit(lambda: ctx.ntt(d_mat, W, n, dif=False))
+    out["ntt_dit_ms"] = round(ms, 3)
+    out["ntt_Gbfly_s"] = round(W * (n // 2) * args.log_rows / ms / 1e6, 1)
     print(json.dumps(out), flush=True)
     for p in (d_mat, d_out, d_nodes):
         ctx.free(p)

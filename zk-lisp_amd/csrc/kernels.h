@@ -111,9 +111,18 @@ void launch_boundary_w(const uint32_t* d_row_start, const fe* d_beta, const fe* 
 void launch_check_zero_range_bitrev(const fe* d_data, size_t N, size_t lo, size_t hi, unsigned* d_flag, hipStream_t s);
 
 // ---- OOD / DEEP / FRI ---------------------------------------------------------
-// out[c] = sum_j coef[c*ld + off + j*stride] * pw[j], for j < n ; two power vectors
-void launch_ood(const fe* d_coef, size_t n_cols, size_t col_stride, size_t elem_stride, size_t n, const fe* d_pw1,
-                const fe* d_pw2, fe* d_out1, fe* d_out2, hipStream_t s);
+// OOD evaluations as dot products with bit-reversed power vectors: for column c and point
+// pt (pw1 / pw2), sum_j coef[base(c) + j * elem_stride] * pw_pt[j], j < n, where base(c) =
+// off[c] (use_off) or c * col_stride; split into `chunks` partial sums per (pt, c).
+struct OodArgs {
+  const fe* coef;
+  size_t col_stride, elem_stride, n;
+  const fe* pw1;
+  const fe* pw2;
+  uint32_t ncols, chunks, use_off;
+  uint32_t off[16];
+};
+void launch_ood(const OodArgs& a, fe* d_partial, hipStream_t s);
 struct DeepParams {
   size_t N;
   uint32_t W, C;

@@ -406,7 +406,14 @@ void launch_grind(fe seed, uint64_t base, uint32_t count, uint32_t bits, unsigne
 // A pass covers global half-sizes H in {S, 2S, .., 2^(r-1) S}.  Group q of 2^r elements:
 // L = q mod S, Hb = q / S, element t at Hb*S*2^r + t*S + L.  4096 elements per workgroup.
 // =====================================================================================
-constexpr int NTT_ELEMS = 2048;  // per workgroup: 34 KB of LDS -> 4 workgroups (16 waves) per CU
+#ifndef NTT_ELEMS_CFG
+#define NTT_ELEMS_CFG 1024
+#endif
+#ifndef NTT_THREADS_CFG
+#define NTT_THREADS_CFG 256
+#endif
+constexpr int NTT_ELEMS = NTT_ELEMS_CFG;      // elements per workgroup (1024: 17 KB of LDS)
+constexpr int NTT_THREADS = NTT_THREADS_CFG;  // threads per workgroup
 
 __device__ __forceinline__ uint32_t bitrev(uint32_t x, int logn) { return logn ? (__brev(x) >> (32 - logn)) : 0; }
 
@@ -464,7 +471,7 @@ void build_mont_table(const fe* w, size_t N, void* d_buf, hipStream_t s) {
 // src[c * (N >> src_logb) + (i >> src_logb)] instead of data, i.e. the blowup copies of the
 // (scaled, bit-reversed) coefficients are generated on load rather than materialised.
 template <bool DIF>
-__global__ __launch_bounds__(256) void ntt_pass_kernel(fe* __restrict__ data, size_t ncols, int logN, int r,
+__global__ __launch_bounds__(NTT_THREADS) void ntt_pass_kernel(fe* __restrict__ data, size_t ncols, int logN, int r,
                                                        int logS, MontTab roots, int logTab, const fe* __restrict__ src,
                                                        int src_logb) {
   __shared__ fe buf[NTT_ELEMS + NTT_ELEMS / 16];
@@ -501,7 +508,7 @@ __global__ __launch_bounds__(256) void ntt_pass_kernel(fe* __restrict__ data, si
     return (col << logN) + ((Hb << logS) << r) + (size_t)t * S + L;
   };
   const size_t Nmask = ((size_t)1 << logN) - 1;
-  for (int e = threadIdx.x; e < NTT_ELEMS; e += 256) {
+  for (int e = threadIdx.x; e < NTT_ELEMS; e += NTT_THREADS) {
     int g = gfast ? (e % G) : (e >> r);
     int t = gfast ? (e / G) : (e & (R - 1));
     bool ok;
@@ -516,7 +523,7 @@ __global__ __launch_bounds__(256) void ntt_pass_kernel(fe* __restrict__ data, si
     const int h = 1 << lh;
     const size_t Hs = (size_t)h << logS;  // global half size: stage table base
     // the four butterflies of a thread are disjoint: load all operands, then compute and store
-    constexpr int BPT = NTT_ELEMS / 2 / 256;
+    constexpr int BPT = NTT_ELEMS / 2 / NTT_THREADS;
     fe x0[BPT], x1[BPT];
     size_t te[BPT];
     int o0[BPT];
@@ -524,7 +531,7 @@ __global__ __launch_bounds__(256) void ntt_pass_kernel(fe* __restrict__ data, si
     for (int i = 0; i < BPT; i++) {
       // groups vary fastest across lanes: consecutive lanes take consecutive L, so the
       // twiddle loads w_(2H)^(k*S + L) are contiguous in the root table
-      const int u = threadIdx.x + 256 * i;
+      const int u = threadIdx.x + NTT_THREADS * i;
       const int g = u % G;
       const int w = u / G;
       const int k = w & (h - 1);
@@ -550,7 +557,7 @@ __global__ __launch_bounds__(256) void ntt_pass_kernel(fe* __restrict__ data, si
     }
     __syncthreads();
   }
-  for (int e = threadIdx.x; e < NTT_ELEMS; e += 256) {
+  for (int e = threadIdx.x; e < NTT_ELEMS; e += NTT_THREADS) {
     int g = gfast ? (e % G) : (e >> r);
     int t = gfast ? (e / G) : (e & (R - 1));
     bool ok;
@@ -572,7 +579,7 @@ static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
       int logS = cur - r + 1;
       size_t groups = (N >> r) * ncols;
       size_t G = NTT_ELEMS >> r;
-      ntt_pass_kernel<true><<<(unsigned)((groups + G - 1) / G), 256, 0, s>>>(d, ncols, logN, r, logS, roots, logTab,
+      ntt_pass_kernel<true><<<(unsigned)((groups + G - 1) / G), NTT_THREADS, 0, s>>>(d, ncols, logN, r, logS, roots, logTab,
                                                                              nullptr, 0);
       cur -= r;
     }
@@ -582,7 +589,7 @@ static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
       int r = std::min(8, hi - cur + 1);
       size_t groups = (N >> r) * ncols;
       size_t G = NTT_ELEMS >> r;
-      ntt_pass_kernel<false><<<(unsigned)((groups + G - 1) / G), 256, 0, s>>>(d, ncols, logN, r, cur, roots, logTab,
+      ntt_pass_kernel<false><<<(unsigned)((groups + G - 1) / G), NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots, logTab,
                                                                               cur == lo ? src : nullptr, src_logb);
       cur += r;
     }
@@ -928,12 +935,15 @@ void launch_check_zero_range_bitrev(const fe* d, size_t N, size_t lo, size_t hi,
 // =====================================================================================
 // OOD (TracePolyTable::get_ood_frame / CompositionPoly ood): dot products with powers
 // =====================================================================================
-__global__ __launch_bounds__(256) void ood_kernel(const fe* coef, size_t col_stride, size_t elem_stride, size_t n,
-                                                  const fe* pw1, const fe* pw2, fe* out1, fe* out2) {
-  const fe* pw = blockIdx.y ? pw2 : pw1;
-  const fe* c = coef + (size_t)blockIdx.x * col_stride;
+// partial[(pt * ncols + c) * chunks + k] = sum over chunk k of coef(c, j) * pw_pt[j]; the
+// host adds the chunk partials (the OOD frame is read back anyway)
+__global__ __launch_bounds__(256) void ood_kernel(OodArgs A, fe* partial) {
+  const uint32_t c = blockIdx.x, pt = blockIdx.y, k = blockIdx.z;
+  const fe* pw = pt ? A.pw2 : A.pw1;
+  const fe* col = A.coef + (A.use_off ? (size_t)A.off[c] : (size_t)c * A.col_stride);
+  const size_t len = A.n / A.chunks, j0 = (size_t)k * len;
   uint32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (size_t j = threadIdx.x; j < n; j += 256) mul_acc(c[j * elem_stride], pw[j], acc);
+  for (size_t j = j0 + threadIdx.x; j < j0 + len; j += 256) mul_acc(col[j * A.elem_stride], pw[j], acc);
   __shared__ fe red[256];
   red[threadIdx.x] = reduce288(acc);
   __syncthreads();
@@ -941,11 +951,10 @@ __global__ __launch_bounds__(256) void ood_kernel(const fe* coef, size_t col_str
     if ((int)threadIdx.x < w) red[threadIdx.x] = fe_add(red[threadIdx.x], red[threadIdx.x + w]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) (blockIdx.y ? out2 : out1)[blockIdx.x] = red[0];
+  if (threadIdx.x == 0) partial[((size_t)pt * A.ncols + c) * A.chunks + k] = red[0];
 }
-void launch_ood(const fe* d_coef, size_t ncols, size_t col_stride, size_t elem_stride, size_t n, const fe* pw1,
-                const fe* pw2, fe* o1, fe* o2, hipStream_t s) {
-  ood_kernel<<<dim3((unsigned)ncols, 2), 256, 0, s>>>(d_coef, col_stride, elem_stride, n, pw1, pw2, o1, o2);
+void launch_ood(const OodArgs& A, fe* d_partial, hipStream_t s) {
+  ood_kernel<<<dim3(A.ncols, 2, A.chunks), 256, 0, s>>>(A, d_partial);
 }
 
 // DEEP composition over the LDE domain (agg/trace.rs:1126-1218 restates the formula):

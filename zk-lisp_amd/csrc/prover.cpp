@@ -339,22 +339,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->kconst.ensure(sizeof(ProofConsts));
   ProofConsts* dK = (ProofConsts*)C->kconst.p;
   upload_air_consts(dK, air.dev, s);
-  fe troot;
-  d2h(C, &troot, C->tree.f() + 1, sizeof(fe));
-  coin.reseed(troot);
-  T.mark(2);
-
-  // ---- 2. composition coefficients (Linear): transition then boundary, one draw each
   const size_t na = air.assertions.size();
-  const size_t ndraw = (size_t)air.n_tc + na;
-  C->draws.ensure((ndraw + 1024) * sizeof(fe));
-  {
-    KScope k(C, KF_MISC);
-    launch_draws(coin.seed, coin.counter, ndraw, C->draws.f(), s);
-  }
-  coin.counter += ndraw;
-  upload_alphas_from_device(dK, C->draws.f(), air.n_tc, s);
-
   // boundary tables: per asserted column c, M_c = coset-LDE of
   // reverse(NTT_n(beta_c)); W likewise from sum_c beta*value.
   std::map<uint32_t, uint32_t> slot_of;
@@ -379,6 +364,21 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   HIPCHECK(hipMemcpyAsync(C->ars.p, rowstart.data(), (n + 1) * 4, hipMemcpyHostToDevice, s));
   C->bvec.ensure((size_t)(nb + 1) * n * sizeof(fe));
   C->bm.ensure((size_t)(nb + 1) * ce * sizeof(fe));
+  fe troot;
+  d2h(C, &troot, C->tree.f() + 1, sizeof(fe));
+  coin.reseed(troot);
+  T.mark(2);
+
+  // ---- 2. composition coefficients (Linear): transition then boundary, one draw each
+  const size_t ndraw = (size_t)air.n_tc + na;
+  C->draws.ensure((ndraw + 1024) * sizeof(fe));
+  {
+    KScope k(C, KF_MISC);
+    launch_draws(coin.seed, coin.counter, ndraw, C->draws.f(), s);
+  }
+  coin.counter += ndraw;
+  upload_alphas_from_device(dK, C->draws.f(), air.n_tc, s);
+
   HIPCHECK(hipMemsetAsync(C->bvec.p, 0, (size_t)(nb + 1) * n * sizeof(fe), s));
   const fe* betas = C->draws.f() + air.n_tc;
   {
@@ -467,17 +467,34 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   // shift, so one pair of bit-reversed power vectors of z/3 and zg/3 serves both
   powers_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(fe_mul(z, inv3), fe_one(), n, logn, pw + 2 * n);
   powers_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(fe_mul(zg, inv3), fe_one(), n, logn, pw + 3 * n);
-  C->oodv.ensure(2 * ((size_t)W + Cc) * sizeof(fe));
+  const uint32_t chunks = n >= 8192 ? 32 : 1;  // parallelism for the few composition columns
+  const size_t n_otr = 2 * (size_t)W * chunks, n_ocp = 2 * (size_t)Cc * chunks;
+  C->oodv.ensure((n_otr + n_ocp) * sizeof(fe));
   fe* dood = C->oodv.f();
+  if (Cc > 16) throw std::runtime_error("internal: more than 16 composition columns");
   {
     KScope k(C, KF_MISC);
-    launch_ood(C->coef.f(), W, n, 1, n, pw + 2 * n, pw + 3 * n, dood, dood + W, s);
-    for (int j = 0; j < Cc; j++)
-      launch_ood(C->ce.f() + bitrev_u((uint32_t)j, loge), 1, 0, ce / n, n, pw + 2 * n, pw + 3 * n,
-                 dood + 2 * W + j, dood + 2 * W + Cc + j, s);
+    OodArgs a{};
+    a.coef = C->coef.f(); a.col_stride = n; a.elem_stride = 1; a.n = n;
+    a.pw1 = pw + 2 * n; a.pw2 = pw + 3 * n; a.ncols = W; a.chunks = chunks; a.use_off = 0;
+    launch_ood(a, dood, s);
+    OodArgs b{};
+    b.coef = C->ce.f(); b.col_stride = 0; b.elem_stride = ce / n; b.n = n;
+    b.pw1 = pw + 2 * n; b.pw2 = pw + 3 * n; b.ncols = (uint32_t)Cc; b.chunks = chunks; b.use_off = 1;
+    for (int j = 0; j < Cc; j++) b.off[j] = bitrev_u((uint32_t)j, loge);
+    launch_ood(b, dood + n_otr, s);
   }
-  std::vector<fe> hood(2 * ((size_t)W + Cc));
-  d2h(C, hood.data(), dood, hood.size() * sizeof(fe));
+  std::vector<fe> part(n_otr + n_ocp), hood(2 * ((size_t)W + Cc), fe_zero());
+  d2h(C, part.data(), dood, part.size() * sizeof(fe));
+  // hood = t(z) [W] | t(zg) [W] | chat(z) [Cc] | chat(zg) [Cc]
+  for (size_t pt = 0; pt < 2; pt++) {
+    for (uint32_t c = 0; c < W; c++)
+      for (uint32_t k = 0; k < chunks; k++)
+        hood[pt * W + c] = fe_add(hood[pt * W + c], part[(pt * W + c) * chunks + k]);
+    for (int j = 0; j < Cc; j++)
+      for (uint32_t k = 0; k < chunks; k++)
+        hood[2 * W + pt * Cc + j] = fe_add(hood[2 * W + pt * Cc + j], part[n_otr + (pt * Cc + j) * chunks + k]);
+  }
   std::vector<fe> tz(hood.begin(), hood.begin() + W), tzg(hood.begin() + W, hood.begin() + 2 * W);
   std::vector<fe> hz(Cc), hzg(Cc);
   for (int j = 0; j < Cc; j++) {
