@@ -21,9 +21,14 @@ def _gpu_opts(zkl_hip, o):
 
 @pytest.mark.parametrize("log_n,q,blowup,grind", [
     (5, 8, 16, 0), (5, 64, 16, 8), (6, 32, 8, 4), (8, 64, 16, 10), (10, 64, 16, 12), (9, 20, 32, 6),
+    (5, 1, 16, 0),      # a single query
+    (5, 255, 8, 2),     # maximum queries on a 256-point domain: heavy position collisions
+    (6, 16, 64, 3),     # blowup 64
+    (11, 32, 16, 14),   # long grinding search
 ])
 def test_proof_bytes_match_oracle(oracle, gpu_ctx, log_n, q, blowup, grind):
     import zkl_hip
+    oracle.set_threads(16 if log_n >= 10 else 1)
     n = 1 << log_n
     t, pi, w = zkl_hip.synth_vm_segment(0x5EED0001 + log_n, log_n)
     opts = zkl_hip.proof_options(w, n, queries=q, blowup=blowup, grind=grind)
@@ -33,6 +38,8 @@ def test_proof_bytes_match_oracle(oracle, gpu_ctx, log_n, q, blowup, grind):
     want = oracle.prove(ot, w, n, opi, oo)
     assert len(got) == len(want)
     assert got == want
+    rc, err = oracle.verify(got, opi, oo)
+    assert rc == 0, err
 
 
 def test_multi_partition_parity(oracle, gpu_ctx):
@@ -213,3 +220,27 @@ def test_concurrent_contexts_same_device(gpu_ctx):
     for c in ctxs:
         c.close()
     assert got == want
+
+
+@pytest.mark.parametrize("change,msg", [
+    (dict(log_n=4), "power of two >= 32"),
+    (dict(blowup=4), "blowup factor below"),
+    (dict(blowup=12), "power of two"),
+    (dict(queries=0), "num_queries"),
+    (dict(field_extension=2), "FieldExtension::None"),
+    (dict(width_delta=1), "width"),
+])
+def test_invalid_requests_rejected(gpu_ctx, change, msg):
+    """Unsupported or inconsistent requests fail with ZKL_E_INVALID and a message, never a
+    proof (the reference maps such failures to prove::Error, prove.rs:225-227)."""
+    import zkl_hip
+    log_n = change.get("log_n", 6)
+    t, pi, w = zkl_hip.synth_vm_segment(0x5EED0300, max(log_n, 5))
+    n = 1 << log_n
+    opts = zkl_hip.proof_options(w, 1 << max(log_n, 5), queries=change.get("queries", 8),
+                                 blowup=change.get("blowup", 16), grind=0)
+    if "field_extension" in change:
+        opts.field_extension = change["field_extension"]
+    w_req = w - change.get("width_delta", 0)
+    with pytest.raises(zkl_hip.ZklError, match=msg):
+        gpu_ctx.prove_segment(t, w_req, n, pi, opts)
