@@ -26,7 +26,13 @@ sys.path.insert(0, os.path.join(ROOT, "zk-lisp_amd"))
 
 METRIC = "segment-proofs/sec at 65536 rows, blowup=16; proof bytes bit-exact vs CPU ref"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-MAD_PEAK_GPS = 34188.0         # measured v_mad_u64_u32 rate (profiles/r01/intbench.txt), G/s
+# VALU issue peak: one wave64 VALU instruction per quad-cycle per SIMD (SQ_ACTIVE_INST_VALU
+# counts one quad-cycle per instruction for this kernel's 64-bit integer mix), 256 CUs x 4
+# SIMDs x 2.4 GHz / 4
+VALU_ISSUE_PEAK_G = 256 * 4 * 2.4 / 4   # G wave-instructions/s
+# VALU wave-instructions per Poseidon permutation of the lane-group kernel, from
+# SQ_INSTS_VALU / permutations (profiles/r01/pmc_sq_stagebench.json)
+VALU_INSTR_PER_PERM = 2617
 
 
 def log(*a):
@@ -58,7 +64,7 @@ def perm_model(n, W=204, C=7, blowup=16, parts=None, grind=16, n_tc=193, queries
     return {"trace_rows": N * row, "total": total, "row_perms": row}
 
 
-MADS_PER_PERM = 27 * (144 + 24) * 16  # 32x32->64 multiply-adds of the schoolbook f128 products
+MULMODS_PER_PERM = 27 * (144 + 24)  # f128 multiplications of one permutation (12 cubes x 2 + 144 MDS)
 
 
 def cpu_baseline(log_n_sample, log_n_target):
@@ -209,7 +215,8 @@ def main():
         achieved = alg_bytes / (per_launch_ms * 1e-3) / 1e9
         pm = perm_model(n)
         perms_per_launch = N * pm["row_perms"]  # fused: partitions + merge_many per row
-        mads_per_s = perms_per_launch * MADS_PER_PERM / (per_launch_ms * 1e-3) / 1e9
+        perms_per_s = perms_per_launch / (per_launch_ms * 1e-3)
+        valu_g = perms_per_s * VALU_INSTR_PER_PERM / 1e9
         traffic = load_traffic("hash_rows_kernel<0>")
         out = {
             "metric": METRIC,
@@ -241,15 +248,19 @@ def main():
                 "traffic": traffic,
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": round(per_launch_ms, 3),
-                "note": "integer-VALU bound by construction (SURVEY 0.8); see roofline_valu",
+                "note": "VALU-issue bound (integer Poseidon); see roofline_valu",
             },
             "roofline_valu": {
-                "bound": "valu",
-                "achieved": round(mads_per_s, 1),
-                "peak": MAD_PEAK_GPS,
-                "unit": "G v_mad_u64_u32-equiv/s",
-                "frac": round(mads_per_s / MAD_PEAK_GPS, 4),
+                "bound": "valu-issue",
+                "kernel": "hash_rows_kernel<0>",
+                "achieved": round(valu_g, 1),
+                "peak": VALU_ISSUE_PEAK_G,
+                "unit": "G VALU wave-instructions/s",
+                "frac": round(valu_g / VALU_ISSUE_PEAK_G, 4),
                 "perms_per_launch": perms_per_launch,
+                "perms_per_s": round(perms_per_s),
+                "f128_mulmods_per_s": round(perms_per_s * MULMODS_PER_PERM),
+                "note": "SQ counters show ~98% VALU issue occupancy per SIMD (profiles/r01/pmc_sq_stagebench.json)",
             },
             "dominant_kernel_family": dom,
             "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kacc.items()},

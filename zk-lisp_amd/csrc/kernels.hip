@@ -177,11 +177,13 @@ void upload_hasher_mont(const HasherMont& m, hipStream_t s) {
 // which is what bounds the upper Merkle levels and the FRI layers.
 constexpr int PG_LANES = 12;
 constexpr int PG_PER_WAVE = 5;
-constexpr int PG_WAVE_WORDS = 6 * 60;  // six groups x (5 limbs x 12 lanes)
+constexpr int PG_GROUP_WORDS = 60;  // 5 limbs x 12 lanes
+constexpr int PG_WAVE_WORDS = 6 * PG_GROUP_WORDS;  // six groups
 
 struct PGroup {
   uint32_t m[12][5];  // MDS row j (Montgomery)
   uint32_t* x;        // this group's exchange area: x[limb * 12 + lane]
+
   int j;              // lane within the group
   int g;              // group within the wave (5 = the partial group)
 };
@@ -190,7 +192,8 @@ __device__ __forceinline__ void pg_init(PGroup& P, uint32_t* lds) {
   const int lane = (int)(threadIdx.x & 63);
   P.g = lane / PG_LANES;
   P.j = lane - PG_LANES * P.g;
-  P.x = lds + (threadIdx.x >> 6) * PG_WAVE_WORDS + P.g * 60;
+  P.x = lds + (threadIdx.x >> 6) * PG_WAVE_WORDS + P.g * PG_GROUP_WORDS;
+
 #pragma unroll
   for (int k = 0; k < 12; k++)
 #pragma unroll
@@ -218,11 +221,11 @@ __device__ __forceinline__ void pg_permute(PGroup& P, uint32_t s[5]) {
 #pragma unroll
     for (int l = 0; l < 5; l++) P.x[l * 12 + P.j] = t[l];
     wave_sync();
+    uint64_t col[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint4 v[15];  // all twelve cubes of the group, limb-major: v[l*3+q] = limb l of lanes 4q..4q+3
 #pragma unroll
     for (int i = 0; i < 15; i++) v[i] = xv[i];
     __builtin_amdgcn_wave_barrier();
-    uint64_t col[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int q = 0; q < 3; q++) {
       uint32_t a0[5] = {v[q].x, v[3 + q].x, v[6 + q].x, v[9 + q].x, v[12 + q].x};
