@@ -13,7 +13,6 @@ struct HasherConsts {  // PoseidonHasher suite [0;32] + folded domain labels
   fe dom[2];
   fe dom_elems, dom_merge, dom_many, dom_int;
 };
-void upload_hasher_consts(const HasherConsts& h, hipStream_t s);
 
 // Montgomery/26-bit-limb form of the hasher constants used by the device permutation
 // (R = 2^156 mod p; every constant stored as 5 little-endian 26-bit limbs of x*R mod p).
@@ -77,8 +76,6 @@ void launch_broadcast(const fe* d_in, size_t in_col_stride, size_t in_elem_strid
                       size_t n_cols, size_t n, size_t N, const fe* d_scale, fe mult, bool reverse, fe* d_out, hipStream_t s);
 // data[i] *= scale[bitrev(i)] on contiguous columns (post-DIF scaling)
 void launch_scale_bitrev(fe* d_data, size_t n_cols, size_t n, const fe* d_scale, hipStream_t s);
-// d_out[i] = base * w_N^i for i < N via the root table (step = Ntab / N)
-void launch_geometric(fe base, const fe* d_roots, size_t step, size_t N, fe* d_out, hipStream_t s);
 
 // ---- constraint evaluation ---------------------------------------------------
 struct CeParams {

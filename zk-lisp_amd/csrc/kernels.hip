@@ -13,11 +13,7 @@
 
 namespace zkl {
 
-__constant__ HasherConsts c_h;
 
-void upload_hasher_consts(const HasherConsts& h, hipStream_t s) {
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_h), &h, sizeof h, 0, hipMemcpyHostToDevice, s);
-}
 void upload_air_consts(ProofConsts* dK, const AirDevice& a, hipStream_t s) {
   (void)hipMemcpyAsync(&dK->air, &a, sizeof a, hipMemcpyHostToDevice, s);
 }
@@ -646,14 +642,6 @@ void launch_scale_bitrev(fe* d, size_t ncols, size_t n, const fe* scale, hipStre
   scale_bitrev_kernel<<<(unsigned)((n * ncols + 255) / 256), 256, 0, s>>>(d, ncols, n, ilog2s(n), scale);
 }
 
-__global__ void geometric_kernel(fe base, const fe* roots, size_t step, size_t N, fe* out) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= N) return;
-  out[i] = fe_mul(base, roots[i * step]);
-}
-void launch_geometric(fe base, const fe* roots, size_t step, size_t N, fe* out, hipStream_t s) {
-  geometric_kernel<<<(unsigned)((N + 255) / 256), 256, 0, s>>>(base, roots, step, N, out);
-}
 
 // =====================================================================================
 // Constraint evaluation over the CE coset (DefaultConstraintEvaluator restated):

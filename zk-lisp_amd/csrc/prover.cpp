@@ -196,7 +196,6 @@ void upload_hasher(hipStream_t s) {
     hc.dom_elems = H.dom_elems; hc.dom_merge = H.dom_merge; hc.dom_many = H.dom_many; hc.dom_int = H.dom_int;
     hm = make_hasher_mont(hc);
   });
-  upload_hasher_consts(hc, s);
   upload_hasher_mont(hm, s);
 }
 
