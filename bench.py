@@ -67,30 +67,32 @@ def perm_model(n, W=204, C=7, blowup=16, parts=None, grind=16, n_tc=193, queries
 MULMODS_PER_PERM = 27 * (144 + 24)  # f128 multiplications of one permutation (12 cubes x 2 + 144 MDS)
 
 
-def cpu_baseline(log_n_sample, log_n_target):
-    """Oracle (CPU restatement of the reference algorithm), single thread, on a bounded
-    sample: one full proof of the same synthetic segment family at 2^log_n_sample rows,
-    extrapolated to 2^log_n_target rows by the permutation-count work model."""
+def cpu_baseline(log_n_sample, log_n_target, threads):
+    """Oracle (CPU restatement of the reference algorithm) on a bounded sample: one full proof
+    of the same synthetic segment family at 2^log_n_sample rows with `threads` OpenMP
+    threads (row hashing, Merkle levels, LDE columns, constraint evaluation, DEEP, grinding
+    in parallel), extrapolated to 2^log_n_target rows by the permutation-count work model."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as orc
     orc.lib()
-    orc.set_threads(1)
+    orc.set_threads(threads)
     n = 1 << log_n_sample
     t, pi, w = orc.synth_segment(0x5EED0001, log_n_sample)
     opts = orc.default_options(w, n)
     t0 = time.perf_counter()
     orc.prove(t, w, n, pi, opts)
     dt = time.perf_counter() - t0
+    orc.set_threads(1)
     ms, mt = perm_model(n), perm_model(1 << log_n_target)
     per_target = dt * mt["total"] / ms["total"]
     return {
         "value": round(1.0 / per_target, 6),
         "unit": "segment-proofs/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
         "sample": (f"oracle proof of a 2^{log_n_sample}-row synthetic segment (same options) took {dt:.1f}s "
-                   f"single-threaded; scaled x{mt['total'] / ms['total']:.1f} by the Poseidon-permutation work "
-                   f"model to a 2^{log_n_target}-row segment"),
+                   f"with {threads} threads; scaled x{mt['total'] / ms['total']:.2f} by the Poseidon-permutation "
+                   f"work model to a 2^{log_n_target}-row segment"),
         "sample_seconds": round(dt, 2),
     }
 
@@ -154,7 +156,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log-n", type=int, default=16)
-    ap.add_argument("--cpu-sample-log-n", type=int, default=11)
+    ap.add_argument("--cpu-sample-log-n", type=int, default=14)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0: min(16, host CPUs))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c3-segments", type=int, default=8, help="segments for the configs[2] pipeline line (0: skip)")
     ap.add_argument("--c3-inflight", type=str, default="1,2,4", help="contexts in flight to try for configs[2]")
@@ -278,7 +281,8 @@ def main():
                 "unit": "segment-proofs/s"}
         if world == 1 and not args.no_cpu_baseline:
             try:
-                out["cpu_baseline"] = cpu_baseline(args.cpu_sample_log_n, log_n)
+                th = args.cpu_threads or min(16, os.cpu_count() or 1)
+                out["cpu_baseline"] = cpu_baseline(args.cpu_sample_log_n, log_n, th)
             except Exception as e:  # reported, never fatal for the GPU number
                 out["cpu_baseline"] = {"value": None, "error": str(e)}
         print(json.dumps(out), file=result_out, flush=True)

@@ -315,12 +315,18 @@ int orc_prove_segment(const zkl_f128 *trace, uint32_t W, uint32_t n, const zkl_a
   fe *coef = (fe *)malloc((size_t)W * n * sizeof(fe));
   fe *lde = (fe *)malloc(N * W * sizeof(fe)); /* row-major */
   fe *col = (fe *)malloc(N * sizeof(fe));
-  for (uint32_t c = 0; c < W; c++) {
-    fe *cc = coef + (size_t)c * n;
-    for (size_t r = 0; r < n; r++) cc[r] = fe_of(trace[(size_t)c * n + r]);
-    ntt_inplace(cc, n, 1);
-    coset_evaluate(cc, n, col, N, offset);
-    for (size_t r = 0; r < N; r++) lde[r * W + c] = col[r];
+#pragma omp parallel num_threads(g_orc_threads)
+  {
+    fe *colt = (fe *)malloc(N * sizeof(fe));
+#pragma omp for schedule(dynamic, 1)
+    for (uint32_t c = 0; c < W; c++) {
+      fe *cc = coef + (size_t)c * n;
+      for (size_t r = 0; r < n; r++) cc[r] = fe_of(trace[(size_t)c * n + r]);
+      ntt_inplace(cc, n, 1);
+      coset_evaluate(cc, n, colt, N, offset);
+      for (size_t r = 0; r < N; r++) lde[r * W + c] = colt[r];
+    }
+    free(colt);
   }
   double t1 = now_ms();
   fe *leaves = (fe *)malloc(N * sizeof(fe));
