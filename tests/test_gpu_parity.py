@@ -244,3 +244,23 @@ def test_invalid_requests_rejected(gpu_ctx, change, msg):
     w_req = w - change.get("width_delta", 0)
     with pytest.raises(zkl_hip.ZklError, match=msg):
         gpu_ctx.prove_segment(t, w_req, n, pi, opts)
+
+
+@pytest.mark.slow
+def test_c5_shape_2p20_rows_verifies(oracle, gpu_ctx):
+    """BASELINE configs[4] shape: one 2^20-row segment (LDE 2^24 x 204 = 55 GB in HBM,
+    partitions (16,16) -> 13 row partitions).  The oracle prover is too slow at this size,
+    so the proof is checked by the oracle verifier (plus a one-byte corruption)."""
+    import zkl_hip
+    oracle.set_threads(16)
+    n = 1 << 20
+    t, pi, w = zkl_hip.synth_vm_segment(0x5EED0020, 20)
+    opts = zkl_hip.proof_options(w, n)
+    assert (opts.num_partitions, opts.hash_rate) == (16, 16)
+    proof = gpu_ctx.prove_segment(t, w, n, pi, opts)
+    print("2^20 proof", len(proof), gpu_ctx.stage_times())
+    oo = oracle.ProofOptions(*[getattr(opts, f) for f, _ in opts._fields_])
+    _, opi, _ = oracle.synth_segment(0x5EED0020, 20)
+    rc, err = oracle.verify(proof, opi, oo)
+    oracle.set_threads(1)
+    assert rc == 0, err
