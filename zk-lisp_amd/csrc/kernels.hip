@@ -273,6 +273,128 @@ __device__ __forceinline__ fe pg_bcast(const PGroup& P, fe v, int src) {
   return r;
 }
 
+// ---- wide lane groups (latency-bound levels) ------------------------------------------
+// 24 lanes per state: lane (e, h) owns state element e (both halves hold it) and the MDS
+// row-e constants of columns 6h..6h+5; each half sums six products and the halves add
+// their 64-bit column sums through LDS before the (redundant) REDC.  Two states per wave
+// (lanes 48..63 idle).  A round issues ~345 instead of ~518 instructions per lane, so a
+// permutation finishes ~1.5x sooner; used where a level has too few states to fill the
+// SIMDs (upper Merkle levels, small FRI layers, the FRI transcript).
+constexpr int PW_PER_WAVE = 2;
+constexpr int PW_GROUP_WORDS = 60 + 24 * 20;  // cubes [l][12] + partial columns [h*12+e][20]
+constexpr int PW_WAVE_WORDS = 3 * PW_GROUP_WORDS;
+
+struct PWGroup {
+  uint32_t m[6][5];  // MDS row e, columns 6h..6h+5 (Montgomery)
+  uint32_t* x;       // cubes: x[limb * 12 + e]
+  uint32_t* y;       // partial column sums: y[(h * 12 + e) * 20 + w]
+  int e, h, g;
+};
+
+__device__ __forceinline__ void pw_init(PWGroup& P, uint32_t* lds) {
+  const int lane = (int)(threadIdx.x & 63);
+  P.g = lane / 24;
+  const int j24 = lane - 24 * P.g;
+  P.h = j24 / 12;
+  P.e = j24 - 12 * P.h;
+  P.x = lds + (threadIdx.x >> 6) * PW_WAVE_WORDS + P.g * PW_GROUP_WORDS;
+  P.y = P.x + 60;
+#pragma unroll
+  for (int k = 0; k < 6; k++)
+#pragma unroll
+    for (int l = 0; l < 5; l++) P.m[k][l] = c_hm.mds[P.e][6 * P.h + k][l];
+}
+
+__device__ __forceinline__ void pw_permute(PWGroup& P, uint32_t s[5]) {
+  const uint32_t* rcp = &c_hm.rc[0][P.e][0];
+  uint4* ymine = reinterpret_cast<uint4*>(P.y + (P.h * 12 + P.e) * 20);
+  const uint4* yother = reinterpret_cast<const uint4*>(P.y + ((1 - P.h) * 12 + P.e) * 20);
+#pragma unroll 1
+  for (int r = 0; r < 27; r++, rcp += 60) {
+    uint32_t rc[5];
+#pragma unroll
+    for (int l = 0; l < 5; l++) rc[l] = rcp[l];
+    uint32_t t[5];
+    mont_cube(s, t);
+    if (P.h == 0) {
+#pragma unroll
+      for (int l = 0; l < 5; l++) P.x[l * 12 + P.e] = t[l];
+    }
+    wave_sync();
+    uint32_t tk[6][5];
+#pragma unroll
+    for (int l = 0; l < 5; l++) {
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        const uint2 w = *reinterpret_cast<const uint2*>(P.x + l * 12 + 6 * P.h + 2 * q);
+        tk[2 * q][l] = w.x;
+        tk[2 * q + 1][l] = w.y;
+      }
+    }
+    uint64_t col[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 6; k++) mac5(tk[k], P.m[k], col);
+#pragma unroll
+    for (int q = 0; q < 5; q++)
+      ymine[q] = make_uint4((uint32_t)col[2 * q], (uint32_t)(col[2 * q] >> 32), (uint32_t)col[2 * q + 1],
+                            (uint32_t)(col[2 * q + 1] >> 32));
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      const uint4 o = yother[q];
+      col[2 * q] += ((uint64_t)o.y << 32) | o.x;
+      col[2 * q + 1] += ((uint64_t)o.w << 32) | o.z;
+    }
+    __builtin_amdgcn_wave_barrier();
+    redc(col, s);
+#pragma unroll
+    for (int l = 0; l < 5; l++) s[l] += rc[l];
+  }
+}
+
+template <int D, class Loader>
+__device__ __forceinline__ fe pw_sponge(PWGroup& P, bool live, int nmsg, Loader ld) {
+  uint32_t s[5];
+#pragma unroll
+  for (int l = 0; l < 5; l++)
+    s[l] = P.e == 0 ? c_hm.dfe[D][l] : P.e == 10 ? c_hm.dom[0][l] : P.e == 11 ? c_hm.dom[1][l] : 0u;
+  const int T = nmsg + 1;
+  for (int b = 0; b * 10 < T; b++) {
+    const int idx = b * 10 + P.e;
+    if (live && P.e < 10 && idx >= 1 && idx < T) {
+      uint32_t m[5];
+      to_mont(ld(idx - 1), m);
+#pragma unroll
+      for (int l = 0; l < 5; l++) s[l] += m[l];
+    }
+    pw_permute(P, s);
+  }
+  return from_mont(s);  // state element 0 in lanes with e == 0
+}
+
+__device__ __forceinline__ fe pw_bcast(const PWGroup& P, fe v, int src_e) {
+  const int from = 24 * P.g + src_e;
+  fe r;
+  r.lo = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v.lo >> 32), from) << 32) | (uint32_t)__shfl((int)(uint32_t)v.lo, from);
+  r.hi = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v.hi >> 32), from) << 32) | (uint32_t)__shfl((int)(uint32_t)v.hi, from);
+  return r;
+}
+
+#define PW_SETUP()                                            \
+  __shared__ __align__(16) uint32_t pw_lds[4 * PW_WAVE_WORDS]; \
+  PWGroup P;                                                  \
+  pw_init(P, pw_lds);                                         \
+  const size_t item = ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * PW_PER_WAVE + (size_t)P.g;
+
+static inline unsigned pw_blocks(size_t items) {
+  const size_t per = 4 * PW_PER_WAVE;
+  return (unsigned)((items + per - 1) / per);
+}
+
+// levels (and FRI layers) with at most this many states use the wide groups: up to one
+// wide wave per SIMD, where per-state latency rather than issue throughput bounds the level
+constexpr size_t PW_MAX_ITEMS = 2048;
+
 // Occupancy target of the lane-group kernels: 2 waves/SIMD lets the scheduler batch the 15
 // LDS reads of a round; 3 forces them to serialise on a shared register window.
 #ifndef PG_WAVES
@@ -366,22 +488,35 @@ void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np
     hash_rows_kernel<0><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, d_out);
 }
 
+__global__ __launch_bounds__(256) void merkle_level_wide_kernel(fe* nodes, size_t lvl) {
+  PW_SETUP();
+  const bool live = P.g < PW_PER_WAVE && item < lvl;
+  const size_t i = lvl + (live ? item : 0);
+  fe d = pw_sponge<DOM_MERGE>(P, live, 2, [&](int j) { return nodes[2 * i + j]; });
+  if (live && P.e == 0 && P.h == 0) nodes[i] = d;
+}
+
 void launch_merkle(fe* d_nodes, size_t n, hipStream_t s) {
-  for (size_t lvl = n / 2; lvl >= 1; lvl /= 2) merkle_level_kernel<<<pg_blocks(lvl), 256, 0, s>>>(d_nodes, lvl);
+  for (size_t lvl = n / 2; lvl >= 1; lvl /= 2) {
+    if (lvl <= PW_MAX_ITEMS)
+      merkle_level_wide_kernel<<<pw_blocks(lvl), 256, 0, s>>>(d_nodes, lvl);
+    else
+      merkle_level_kernel<<<pg_blocks(lvl), 256, 0, s>>>(d_nodes, lvl);
+  }
 }
 
 // FRI transcript step on the device (DefaultRandomCoin: reseed with the layer root, then
 // draw alpha with counter 1): coin[0] = merge(coin[0], root); coin[1] = merge_with_int(
 // coin[0], 1); the root is also copied to *root_out.  One wave, group 0.
 __global__ __launch_bounds__(64) void fri_coin_kernel(fe* coin, const fe* root, fe* root_out) {
-  __shared__ __align__(16) uint32_t pg_lds[PG_WAVE_WORDS];
-  PGroup P;
-  pg_init(P, pg_lds);
+  __shared__ __align__(16) uint32_t pw_lds[PW_WAVE_WORDS];
+  PWGroup P;
+  pw_init(P, pw_lds);
   const bool live = P.g == 0;
   const fe seed = coin[0], r = *root;
-  fe s1 = pg_sponge<DOM_MERGE>(P, live, 2, [&](int j) { return j == 0 ? seed : r; });
-  s1 = pg_bcast(P, s1, 0);
-  fe a = pg_sponge<DOM_INT>(P, live, 2, [&](int j) { return j == 0 ? s1 : fe{1, 0}; });
+  fe s1 = pw_sponge<DOM_MERGE>(P, live, 2, [&](int j) { return j == 0 ? seed : r; });
+  s1 = pw_bcast(P, s1, 0);
+  fe a = pw_sponge<DOM_INT>(P, live, 2, [&](int j) { return j == 0 ? s1 : fe{1, 0}; });
   if (threadIdx.x == 0) {
     coin[0] = s1;
     coin[1] = a;
@@ -979,9 +1114,19 @@ __global__ PG_KERNEL void fri_leaf_kernel(const fe* ev, size_t half, fe* leaves)
   fe d = pg_sponge<DOM_ELEMS>(P, live, 1, [&](int) { return fold_pair(ev[i], ev[i + half]); });
   if (live && P.j == 0) leaves[i] = d;
 }
+__global__ __launch_bounds__(256) void fri_leaf_wide_kernel(const fe* ev, size_t half, fe* leaves) {
+  PW_SETUP();
+  const bool live = P.g < PW_PER_WAVE && item < half;
+  const size_t i = live ? item : 0;
+  fe d = pw_sponge<DOM_ELEMS>(P, live, 1, [&](int) { return fold_pair(ev[i], ev[i + half]); });
+  if (live && P.e == 0 && P.h == 0) leaves[i] = d;
+}
 void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s) {
   size_t h = Nd / 2;
-  fri_leaf_kernel<<<pg_blocks(h), 256, 0, s>>>(d_ev, h, d_leaves);
+  if (h <= PW_MAX_ITEMS)
+    fri_leaf_wide_kernel<<<pw_blocks(h), 256, 0, s>>>(d_ev, h, d_leaves);
+  else
+    fri_leaf_kernel<<<pg_blocks(h), 256, 0, s>>>(d_ev, h, d_leaves);
 }
 // fold: (v0+v1)/2 + alpha (v0-v1) / (2 x0), x0 = GENERATOR * g_d^i (constant offset, agg/trace.rs:764-800)
 __global__ void fri_fold_kernel(const fe* ev, size_t half, const fe* alpha_p, const fe* iroots, int shift, fe inv3,
