@@ -170,6 +170,11 @@ int zkl_hip_ntt(zkl_ctx* ctx, void* d_data, uint32_t n_cols, uint32_t n, int dif
  * column-major trace (204 x 2^log_n) and the AIR public inputs. */
 int zkl_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128* trace_out,
                          zkl_air_public_inputs* pi_out, uint32_t* width_out);
+/* Same with flags: bit 0 interleaves SAbsorbN / SSqueeze sponge ops (vm/trace/vm.rs:565-672)
+ * so the segment enables FM_VM | FM_SPONGE | FM_POSEIDON and the Poseidon AIR block
+ * (zk-lisp-proof-winterfell/src/air/poseidon.rs:26-162).  flags = 0 is zkl_synth_vm_segment. */
+int zkl_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f128* trace_out,
+                            zkl_air_public_inputs* pi_out, uint32_t* width_out);
 
 #ifdef __cplusplus
 }

@@ -119,7 +119,7 @@ int air_new(zk_air *air, const zkl_air_public_inputs *pi, uint32_t width, size_t
   air->feat_sponge = !!(eff & FM_SPONGE);
   air->feat_merkle = !!(eff & FM_MERKLE);
   air->feat_ram = !!(eff & FM_RAM);
-  if (air->feat_poseidon || air->feat_merkle || air->feat_ram) return -1;
+  if (air->feat_merkle || air->feat_ram) return -1;
   int pid_nz = 0, com_nz = 0;
   for (int i = 0; i < 32; i++) { pid_nz |= pi->program_id[i]; com_nz |= pi->program_commitment[i]; }
   air->rom_enabled = pid_nz != 0;
@@ -138,6 +138,8 @@ int air_new(zk_air *air, const zkl_air_public_inputs *pi, uint32_t width, size_t
   pos_suite_derive(pi->program_id, POS_ROUNDS, &ps);
   air->dom[0] = ps.dom[0];
   air->dom[1] = ps.dom[1];
+  memcpy(air->pose_mds, ps.mds, sizeof air->pose_mds);
+  memcpy(air->pose_rc, ps.rc, sizeof air->pose_rc);
   rom_constants(pi->program_id, air->rom_rc, air->rom_mds);
   rom_w(17, air->rom_w0);
   rom_w(1037, air->rom_w1);
@@ -146,6 +148,15 @@ int air_new(zk_air *air, const zkl_air_public_inputs *pi, uint32_t width, size_t
   /* degrees in module order (mod.rs:217-238) */
   int nd = 0;
   uint32_t m = pi->vm_usage_mask;
+  if (air->feat_poseidon) { /* PoseidonAir::push_degrees (poseidon.rs:26-62) */
+    for (int i = 0; i < POS_ROUNDS * 12; i++) air->deg_base[nd++] = 4;
+    for (int i = 0; i < 12; i++) air->deg_base[nd++] = 1;
+    air->pose_bind = air->feat_vm && air->feat_sponge && (m & (1u << U_SPONGE));
+    if (air->pose_bind) {
+      static const int lane_bases[10] = {6, 6, 3, 3, 3, 3, 3, 3, 3, 3};
+      for (int i = 0; i < 10; i++) air->deg_base[nd++] = lane_bases[i];
+    }
+  }
   if (air->feat_vm) {
     for (int i = 0; i < 5 * NR; i++) air->deg_base[nd++] = 2;
     for (int i = 0; i < 5; i++) air->deg_base[nd++] = 1;
@@ -298,6 +309,43 @@ void air_eval_transition(const zk_air *air, const fe *cur, const fe *nxt, const 
   fe g_carry = fe_add(p_map, fe_sub(p_pad, p_pad_last));
   for (int j = 0; j < POS_ROUNDS - 1; j++) g_carry = fe_add(g_carry, per[1 + j]);
   fe rom_on = air->commit_nonzero ? 1 : 0;
+
+  if (air->feat_poseidon) {
+    /* ---------------- PoseidonAir (poseidon.rs:65-162) ---------------- */
+    const fe pa = cur[c->pose_active];
+    fe s3[12], ms[12];
+    for (int i = 0; i < 12; i++) s3[i] = fe_cube(cur[c->lanes_start + i]);
+    for (int i = 0; i < 12; i++) {
+      fe acc = 0;
+      for (int k = 0; k < 12; k++) acc = fe_add(acc, fe_mul(air->pose_mds[i][k], s3[k]));
+      ms[i] = acc;
+    }
+    for (int j = 0; j < POS_ROUNDS; j++) {
+      fe g = fe_mul(pa, per[1 + j]);
+      for (int i = 0; i < 12; i++)
+        res[ix++] = fe_mul(g, fe_sub(nxt[c->lanes_start + i], fe_add(ms[i], air->pose_rc[j][i])));
+    }
+    fe g_hold = fe_sub(p_pad, p_pad_last);
+    for (int i = 0; i < 12; i++) res[ix++] = fe_mul(g_hold, fe_sub(nxt[c->lanes_start + i], cur[c->lanes_start + i]));
+    if (air->pose_bind) {
+      fe b_sponge = cur[c->op[8]];
+      for (int lane = 0; lane < 10; lane++) {
+        fe b0 = cur[c->sel_s_bits + lane * 3], b1 = cur[c->sel_s_bits + lane * 3 + 1],
+           b2 = cur[c->sel_s_bits + lane * 3 + 2], act = cur[c->sel_s_active + lane];
+        const fe *rr = cur + c->r_start;
+        fe nb0 = fe_sub(1, b0), nb1 = fe_sub(1, b1), nb2 = fe_sub(1, b2);
+        fe s0 = fe_add(fe_mul(b0, rr[1]), fe_mul(nb0, rr[0]));
+        fe s1 = fe_add(fe_mul(b0, rr[3]), fe_mul(nb0, rr[2]));
+        fe s2 = fe_add(fe_mul(b0, rr[5]), fe_mul(nb0, rr[4]));
+        fe s3v = fe_add(fe_mul(b0, rr[7]), fe_mul(nb0, rr[6]));
+        fe t0 = fe_add(fe_mul(b1, s1), fe_mul(nb1, s0));
+        fe t1 = fe_add(fe_mul(b1, s3v), fe_mul(nb1, s2));
+        fe sel_val = fe_add(fe_mul(b2, t1), fe_mul(nb2, t0));
+        fe expect = fe_mul(act, sel_val);
+        res[ix++] = fe_mul(fe_mul(fe_mul(p_map, pa), b_sponge), fe_sub(cur[c->lanes_start + lane], expect));
+      }
+    }
+  }
 
   if (air->feat_vm) {
     /* ---------------- VmCtrlAir (ctrl.rs:114-390) ---------------- */

@@ -70,7 +70,7 @@ typedef struct {
 } zk_cols;
 void cols_for_config(int vm, int ram, int sponge, int merkle, int rom, zk_cols *c);
 
-#define MAX_TC 512
+#define MAX_TC 1024
 typedef struct {
   zk_cols cols;
   int feat_poseidon, feat_vm, feat_vm_expect, feat_sponge, feat_merkle, feat_ram, rom_enabled;
@@ -79,6 +79,8 @@ typedef struct {
   fe rom_rc[POS_ROUNDS][3], rom_mds[3][3];
   fe rom_w0[59], rom_w1[59];
   fe dom[2];
+  fe pose_mds[12][12], pose_rc[POS_ROUNDS][12]; /* AIR Poseidon suite (suite_id = program_id) */
+  int pose_bind;                                 /* VM->lane bindings present (poseidon.rs:48-62) */
   fe program_fe[2];
   /* transition constraint degrees (base, has_cycle32) */
   int n_tc;
@@ -100,6 +102,9 @@ void air_periodic_at(const zk_air *air, fe x, fe out[32]);
 /* ---------------- trace generator (vm/trace/ (vm, rom) subset) ---------------- */
 int orc_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128 *trace_out,
                          zkl_air_public_inputs *pi_out, uint32_t *width_out);
+/* flags bit 0: program with SAbsorbN / SSqueeze sponge ops (features VM | SPONGE | POSEIDON) */
+int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f128 *trace_out,
+                            zkl_air_public_inputs *pi_out, uint32_t *width_out);
 
 /* ---------------- prover / verifier ---------------- */
 int orc_prove_segment(const zkl_f128 *trace, uint32_t width, uint32_t n,

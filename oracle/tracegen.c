@@ -26,19 +26,28 @@ static uint64_t splitmix64(uint64_t *s) {
   return z ^ (z >> 31);
 }
 
-enum { OP_CONST = 0, OP_MOV = 1, OP_ADD = 2, OP_SUB = 3, OP_MUL = 4, OP_NEG = 5, OP_END = 99 };
-typedef struct { int kind; int dst, a, b; uint64_t imm; } synth_op;
+enum { OP_CONST = 0, OP_MOV = 1, OP_ADD = 2, OP_SUB = 3, OP_MUL = 4, OP_NEG = 5, OP_ABSORB = 10, OP_SQUEEZE = 11,
+       OP_END = 99 };
+typedef struct { int kind; int dst, a, b; uint64_t imm; int nabs; int abs_regs[3]; } synth_op;
 
-static void synth_program(uint64_t seed, size_t levels, synth_op *ops) {
+/* flags bit 0: sponge program (SAbsorbN / SSqueeze, vm.rs:565-672) interleaved with ALU ops;
+ * every 8 levels: absorb, const, absorb, squeeze, add, mov, mul, squeeze-with-nothing-pending */
+static void synth_program(uint64_t seed, size_t levels, synth_op *ops, uint32_t flags) {
   uint64_t st = seed;
   static const int cyc[4] = {OP_CONST, OP_ADD, OP_MOV, OP_MUL};
+  static const int cyc_s[8] = {OP_ABSORB, OP_CONST, OP_ABSORB, OP_SQUEEZE, OP_ADD, OP_MOV, OP_MUL, OP_SQUEEZE};
   for (size_t l = 0; l + 1 < levels; l++) {
     uint64_t r = splitmix64(&st);
-    ops[l].kind = cyc[l % 4];
+    ops[l].kind = (flags & 1) ? cyc_s[l % 8] : cyc[l % 4];
     ops[l].dst = (int)(r & 7);
     ops[l].a = (int)((r >> 3) & 7);
     ops[l].b = (int)((r >> 6) & 7);
     ops[l].imm = ops[l].kind == OP_CONST ? (splitmix64(&st) >> 1) : 0;
+    ops[l].nabs = 0;
+    if (ops[l].kind == OP_ABSORB) {
+      ops[l].nabs = 1 + (int)((r >> 9) % 3);
+      for (int i = 0; i < 3; i++) ops[l].abs_regs[i] = (int)((r >> (12 + 3 * i)) & 7);
+    }
   }
   ops[levels - 1].kind = OP_END;
   ops[levels - 1].dst = ops[levels - 1].a = ops[levels - 1].b = 0;
@@ -70,6 +79,47 @@ static fe rom_encode_row(const zk_cols *c, const zkl_f128 *t, size_t n, size_t r
 
 int orc_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128 *t, zkl_air_public_inputs *pi,
                          uint32_t *width_out) {
+  return orc_synth_vm_segment_ex(seed, log_n, 0, t, pi, width_out);
+}
+
+/* apply_level_absorb (vm/trace/poseidon.rs:9-87): lanes of one level hold the AIR-suite
+ * permutation of [inputs (<= 10, zero padded), dom0, dom1]: map row = input state, round
+ * row 1+j = state before round j, final and pad rows = output state */
+static void apply_level_absorb(zkl_f128 *t, size_t n, const zk_cols *c, const pos_suite *ps, size_t level,
+                               const fe *in, int nin) {
+  size_t b = level * 32;
+  fe st[12];
+  for (int i = 0; i < 12; i++) st[i] = 0;
+  for (int i = 0; i < nin && i < 10; i++) st[i] = in[i];
+  st[10] = ps->dom[0];
+  st[11] = ps->dom[1];
+  for (int i = 0; i < 12; i++) set_fe(t, n, c->lanes_start + i, b, st[i]);
+  for (int j = 0; j < POS_ROUNDS; j++) {
+    for (int i = 0; i < 12; i++) set_fe(t, n, c->lanes_start + i, b + 1 + j, st[i]);
+    fe s3[12], y[12];
+    for (int i = 0; i < 12; i++) s3[i] = fe_cube(st[i]);
+    for (int i = 0; i < 12; i++) {
+      fe acc = 0;
+      for (int k = 0; k < 12; k++) acc = fe_add(acc, fe_mul(ps->mds[i][k], s3[k]));
+      y[i] = fe_add(acc, ps->rc[j][i]);
+    }
+    memcpy(st, y, sizeof st);
+  }
+  for (size_t r = b + 28; r < b + 32; r++)
+    for (int i = 0; i < 12; i++) set_fe(t, n, c->lanes_start + i, r, st[i]);
+}
+
+static void set_sponge_sel(zkl_f128 *t, size_t n, const zk_cols *c, size_t row, const int *regs, int k) {
+  for (int lane = 0; lane < 10; lane++) {
+    int on = lane < k;
+    int idx = on ? regs[lane] : 0;
+    for (int bit = 0; bit < 3; bit++) set_fe(t, n, c->sel_s_bits + lane * 3 + bit, row, on ? (fe)((idx >> bit) & 1) : 0);
+    set_fe(t, n, c->sel_s_active + lane, row, on ? 1 : 0);
+  }
+}
+
+int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f128 *t, zkl_air_public_inputs *pi,
+                            uint32_t *width_out) {
   if (log_n < 5 || log_n > 26) return -1;
   size_t n = (size_t)1 << log_n, levels = n / 32;
   zk_cols c;
@@ -80,15 +130,19 @@ int orc_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128 *t, zkl_air_pub
   memset(pi, 0, sizeof *pi);
 
   char desc[128];
-  snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 seed=0x%016llx levels=%zu",
-           (unsigned long long)seed, levels);
+  if (flags & 1)
+    snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 sponge seed=0x%016llx levels=%zu",
+             (unsigned long long)seed, levels);
+  else
+    snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 seed=0x%016llx levels=%zu",
+             (unsigned long long)seed, levels);
   uint8_t pid[32];
   orc_blake3((const uint8_t *)desc, strlen(desc), pid);
   pos_suite ps;
   pos_suite_derive(pid, POS_ROUNDS, &ps);
 
   synth_op *ops = (synth_op *)malloc(levels * sizeof(synth_op));
-  synth_program(seed, levels, ops);
+  synth_program(seed, levels, ops, flags);
 
   /* build_empty_trace + pc + dom tags (mod.rs:386-470) */
   for (size_t l = 0; l < levels; l++) {
@@ -102,6 +156,7 @@ int orc_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128 *t, zkl_air_pub
   }
   /* VmTraceBuilder (vm.rs:58-888) */
   fe regs[NR] = {0};
+  int pending[10], npending = 0;
   for (size_t l = 0; l < levels; l++) {
     fe next[NR];
     memcpy(next, regs, sizeof next);
@@ -116,12 +171,36 @@ int orc_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128 *t, zkl_air_pub
       case OP_SUB: onehot = 3; break;
       case OP_MUL: onehot = 4; break;
       case OP_NEG: onehot = 5; break;
+      case OP_ABSORB:
+      case OP_SQUEEZE: onehot = 8; break;
       default: break;
     }
     if (onehot >= 0) set_fe(t, n, c.rom_op_start + onehot, rm, 1);
     for (int i = 0; i < NR; i++) set_fe(t, n, c.r_start + i, rm, regs[i]);
     size_t rows[2] = {rm, rf};
-    for (int q = 0; q < 2 && onehot >= 0; q++) {
+    if (op->kind == OP_ABSORB || op->kind == OP_SQUEEZE) {
+      /* SAbsorbN / SSqueeze (vm.rs:565-672): op_sponge and lane selectors at map and final */
+      int sel_regs[10], k = 0;
+      if (op->kind == OP_ABSORB) {
+        for (int i = 0; i < op->nabs; i++) { sel_regs[k++] = op->abs_regs[i]; pending[npending++] = op->abs_regs[i]; }
+      } else {
+        for (int i = 0; i < npending; i++) sel_regs[k++] = pending[i];
+      }
+      for (int q = 0; q < 2; q++) {
+        set_fe(t, n, c.op[8], rows[q], 1);
+        set_sponge_sel(t, n, &c, rows[q], sel_regs, k);
+      }
+      if (op->kind == OP_SQUEEZE) {
+        set_sel(t, n, rf, c.sel_dst0, op->dst);
+        fe in[10];
+        for (int i = 0; i < k; i++) in[i] = regs[sel_regs[i]];
+        apply_level_absorb(t, n, &c, &ps, l, in, k);
+        next[op->dst] = get_fe(t, n, c.lanes_start, rf);
+        npending = 0;
+        for (size_t r = b; r < b + 32; r++) set_fe(t, n, c.pose_active, r, 1);
+      }
+    }
+    for (int q = 0; q < 2 && onehot >= 0 && onehot != 8; q++) {
       size_t row = rows[q];
       set_fe(t, n, c.op[onehot], row, 1);
       set_sel(t, n, row, c.sel_dst0, op->dst);
@@ -183,8 +262,8 @@ int orc_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128 *t, zkl_air_pub
   /* AIR public inputs (prove.rs:292-423 with segment = whole trace) */
   memcpy(pi->program_id, pid, 32);
   memcpy(pi->program_commitment, pid, 32);
-  pi->feature_mask = 2;          /* FM_VM */
-  pi->segment_feature_mask = 2;
+  pi->feature_mask = (flags & 1) ? 2 | 32 | 1 : 2; /* FM_VM (+ FM_SPONGE | FM_POSEIDON) */
+  pi->segment_feature_mask = pi->feature_mask;
   pi->n_main_slots = 0;
   /* vm_output_from_trace_with_layout (utils.rs:262-289) */
   pi->vm_out_reg = 0; pi->vm_out_row = 29;

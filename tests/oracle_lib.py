@@ -172,14 +172,16 @@ def program_field_commitment(b32: bytes):
     return fe_from(ob[:16]), fe_from(ob[16:])
 
 
-def synth_segment(seed: int, log_n: int):
-    """Returns (trace as (F128 * (W*n)) column-major, AirPublicInputs, W)."""
+def synth_segment(seed: int, log_n: int, flags: int = 0):
+    """Returns (trace as (F128 * (W*n)) column-major, AirPublicInputs, W).
+    flags bit 0: program with sponge ops (features VM | SPONGE | POSEIDON)."""
     w = C.c_uint32()
-    lib().orc_synth_vm_segment(C.c_uint64(seed), C.c_uint32(log_n), None, None, C.byref(w))
+    lib().orc_synth_vm_segment_ex(C.c_uint64(seed), C.c_uint32(log_n), C.c_uint32(flags), None, None, C.byref(w))
     n = 1 << log_n
     trace = (F128 * (w.value * n))()
     pi = AirPublicInputs()
-    rc = lib().orc_synth_vm_segment(C.c_uint64(seed), C.c_uint32(log_n), trace, C.byref(pi), C.byref(w))
+    rc = lib().orc_synth_vm_segment_ex(C.c_uint64(seed), C.c_uint32(log_n), C.c_uint32(flags), trace, C.byref(pi),
+                                       C.byref(w))
     assert rc == 0
     return trace, pi, w.value
 

@@ -37,11 +37,12 @@ def test_select_partitions():
         assert zkl_hip.select_partitions_for_trace(w, n) == exp
 
 
+@pytest.mark.parametrize("flags", [0, 1])
 @pytest.mark.parametrize("log_n", [5, 6, 8, 10, 12])
-def test_product_tracegen_matches_oracle(oracle, log_n):
+def test_product_tracegen_matches_oracle(oracle, log_n, flags):
     import zkl_hip
-    t1, pi1, w1 = zkl_hip.synth_vm_segment(0x5EED0001 + log_n, log_n)
-    t2, pi2, w2 = oracle.synth_segment(0x5EED0001 + log_n, log_n)
+    t1, pi1, w1 = zkl_hip.synth_vm_segment(0x5EED0001 + log_n, log_n, flags)
+    t2, pi2, w2 = oracle.synth_segment(0x5EED0001 + log_n, log_n, flags)
     assert w1 == w2 == 204
     assert bytes(t1) == bytes(t2)
     assert bytes(pi1) == bytes(pi2)

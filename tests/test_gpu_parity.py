@@ -42,6 +42,53 @@ def test_proof_bytes_match_oracle(oracle, gpu_ctx, log_n, q, blowup, grind):
     assert rc == 0, err
 
 
+@pytest.mark.parametrize("log_n,q,blowup,grind", [
+    (5, 8, 16, 0), (6, 32, 8, 4), (8, 64, 16, 10), (10, 64, 16, 12), (7, 255, 4, 1),
+])
+def test_sponge_proof_bytes_match_oracle(oracle, gpu_ctx, log_n, q, blowup, grind):
+    """Segments with SAbsorbN / SSqueeze enable the Poseidon AIR block (poseidon.rs:26-162):
+    27x12 round constraints, 12 hold constraints and the VM->lane bindings (degree 6/3)."""
+    import zkl_hip
+    oracle.set_threads(16 if log_n >= 10 else 1)
+    n = 1 << log_n
+    seed = 0x5B0A6E00 + log_n
+    t, pi, w = zkl_hip.synth_vm_segment(seed, log_n, 1)
+    assert pi.segment_feature_mask == zkl_hip.FM_VM | zkl_hip.FM_SPONGE | zkl_hip.FM_POSEIDON
+    opts = zkl_hip.proof_options(w, n, queries=q, blowup=blowup, grind=grind)
+    got = gpu_ctx.prove_segment(t, w, n, pi, opts)
+    ot, opi, _ = oracle.synth_segment(seed, log_n, 1)
+    oo = oracle.ProofOptions(*[getattr(opts, f) for f, _ in opts._fields_])
+    want = oracle.prove(ot, w, n, opi, oo)
+    oracle.set_threads(1)
+    assert got == want
+    rc, err = oracle.verify(got, opi, oo)
+    assert rc == 0, err
+
+
+def test_sponge_bad_lane_rejected(gpu_ctx):
+    """A Poseidon lane value off its permutation breaks a round constraint."""
+    import zkl_hip
+    n = 1 << 7
+    t, pi, w = zkl_hip.synth_vm_segment(0x5B0A6E07, 7, 1)
+    t[3 * n + 32 * 3 + 9].lo ^= 1      # lane 3, round row 8 of level 3 (a squeeze level)
+    opts = zkl_hip.proof_options(w, n, queries=8, grind=0)
+    with pytest.raises(zkl_hip.ZklError, match="degree too large"):
+        gpu_ctx.prove_segment(t, w, n, pi, opts)
+
+
+def test_sponge_full_size_verifies(oracle, gpu_ctx):
+    """configs[1] shape (2^16 rows, blowup 16, q 64, grind 16) with the Poseidon block on."""
+    import zkl_hip
+    n = 1 << 16
+    t, pi, w = zkl_hip.synth_vm_segment(0x5B0A6E10, 16, 1)
+    opts = zkl_hip.proof_options(w, n)
+    got = gpu_ctx.prove_segment(t, w, n, pi, opts)
+    oo = oracle.ProofOptions(*[getattr(opts, f) for f, _ in opts._fields_])
+    _, opi, _ = oracle.synth_segment(0x5B0A6E10, 16, 1)
+    rc, err = oracle.verify(got, opi, oo)
+    assert rc == 0, err
+
+
 def test_multi_partition_parity(oracle, gpu_ctx):
     """n = 2^14 exercises 2-way row partitioning + merge_many (PartitionOptions)."""
     import zkl_hip

@@ -27,3 +27,34 @@ def test_corrupted_trace_detected(oracle):
     opts = oracle.default_options(w, n, queries=8, grind=0)
     with pytest.raises(RuntimeError, match="degree too large"):
         oracle.prove(t, w, n, pi, opts)
+
+
+def test_sponge_trace_satisfies_poseidon_block(oracle):
+    """Programs with SAbsorbN / SSqueeze (features VM | SPONGE | POSEIDON): the PoseidonAir
+    block (poseidon.rs:65-162: 27x12 round, 12 hold, 10 VM->lane binding constraints, first
+    in evaluation order) holds on the generated trace, and corruptions inside the block's
+    reach are caught by it."""
+    n = 256
+    t, pi, w = oracle.synth_segment(0x5EED0055, 8, 1)
+    assert pi.feature_mask == 0x23 and pi.vm_usage_mask & 0x80
+    assert oracle.check_trace(t, pi, w, n) == (0, 0, 0)
+    # level 3 is a squeeze (cycle absorb, const, absorb, squeeze, ...): round row of round 5
+    row = 3 * 32 + 1 + 5
+    t[5 * n + row + 1].lo ^= 1            # lane 5 of the next state
+    rc, bad_row, idx = oracle.check_trace(t, pi, w, n)
+    assert rc == 1 and bad_row == row and idx < 27 * 12
+    t[5 * n + row + 1].lo ^= 1
+    # a map-row absorb lane that does not match the selected register: binding constraint
+    lane0 = 3 * 32
+    t[0 * n + lane0].lo ^= 2
+    rc, bad_row, idx = oracle.check_trace(t, pi, w, n)
+    assert rc == 1 and 27 * 12 + 12 <= idx < 27 * 12 + 22
+
+
+def test_sponge_trace_proves_and_verifies(oracle):
+    n = 1 << 7
+    t, pi, w = oracle.synth_segment(0x5EED0056, 7, 1)
+    opts = oracle.default_options(w, n, queries=16, grind=4)
+    proof = oracle.prove(t, w, n, pi, opts)
+    rc, err = oracle.verify(proof, pi, opts)
+    assert rc == 0, err

@@ -74,8 +74,8 @@ std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n,
   uint64_t eff = pi.segment_feature_mask ? pi.segment_feature_mask : pi.feature_mask;
   bool f_pose = eff & FM_POSEIDON, f_vm = eff & FM_VM, f_exp = eff & FM_VM_EXPECT, f_sponge = eff & FM_SPONGE,
        f_merkle = eff & FM_MERKLE, f_ram = eff & FM_RAM;
-  if (f_pose || f_merkle || f_ram)
-    return "segment feature mask enables Poseidon/RAM/Merkle AIR blocks, which this backend does not implement yet";
+  if (f_merkle || f_ram)
+    return "segment feature mask enables RAM/Merkle AIR blocks, which this backend does not implement yet";
   bool pid_nz = false, com_nz = false;
   for (int i = 0; i < 32; i++) { pid_nz |= pi.program_id[i] != 0; com_nz |= pi.program_commitment[i] != 0; }
   Layout base = make_layout(true, true, true, true, true);
@@ -97,10 +97,21 @@ std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n,
   PoseidonSuite ps = derive_poseidon_suite(pi.program_id, 27);
   A.suite_dom[0] = ps.dom[0];
   A.suite_dom[1] = ps.dom[1];
+  d.pose_block = f_pose;
+  d.pose_bind = f_pose && f_vm && f_sponge && (m & (1u << U_SPONGE));
+  for (int i = 0; i < 12; i++)
+    for (int k = 0; k < 12; k++) d.pose_mds[i][k] = ps.mds[i][k];
+  for (int r = 0; r < 27; r++)
+    for (int i = 0; i < 12; i++) d.pose_rc[r][i] = ps.rc[r][i];
 
-  // degrees in module order: Ctrl, ALU (vm), ROM (vm/air/mod.rs:217-238)
+  // degrees in module order: Poseidon, Ctrl, ALU (vm), ROM (vm/air/mod.rs:217-238)
   auto& deg = A.degree_base;
   auto push = [&](int cnt, int b) { for (int i = 0; i < cnt; i++) deg.push_back(b); };
+  if (f_pose) {  // PoseidonAir::push_degrees (poseidon.rs:26-62)
+    push(27 * 12, 4);
+    push(12, 1);
+    if (d.pose_bind) { push(2, 6); push(8, 3); }
+  }
   if (f_vm) {
     push(5 * NR, 2); push(5, 1); push(NR, 2);
     if (d.sponge_block) push(40, 2);

@@ -24,7 +24,10 @@ Layout make_layout(bool vm, bool ram, bool sponge, bool merkle, bool rom);
 struct AirDevice {
   Layout cols;
   int feat_vm, sponge_block, commit_nonzero, n_tc;
+  int pose_block, pose_bind;  // PoseidonAir present; its VM->lane bindings present
   uint32_t vm_usage_mask;
+  fe pose_mds[12][12];  // AIR Poseidon suite (suite_id = program_id, vm/air/mod.rs:129-137)
+  fe pose_rc[27][12];
   fe rom_mds[3][3];
   fe rom_rc[27][3];
   fe rom_w0[59];

@@ -22,26 +22,6 @@ __host__ __device__ inline fe fe_one() { return fe{1, 0}; }
 __host__ __device__ inline bool fe_is_zero(fe a) { return (a.lo | a.hi) == 0; }
 __host__ __device__ inline bool fe_eq(fe a, fe b) { return a.lo == b.lo && a.hi == b.hi; }
 
-#ifdef FE_ADD_U128
-__host__ __device__ inline fe fe_add(fe a, fe b) {
-  typedef unsigned __int128 u128;
-  const u128 A = ((u128)a.hi << 64) | a.lo, B = ((u128)b.hi << 64) | b.lo;
-  const u128 P = ((u128)P_HI << 64) | P_LO;
-  const u128 s = A + B;
-  const bool carry = s < A;
-  const u128 t = s - P;
-  const u128 r = (carry || s >= P) ? t : s;
-  return fe{(uint64_t)r, (uint64_t)(r >> 64)};
-}
-__host__ __device__ inline fe fe_sub(fe a, fe b) {
-  typedef unsigned __int128 u128;
-  const u128 A = ((u128)a.hi << 64) | a.lo, B = ((u128)b.hi << 64) | b.lo;
-  const u128 P = ((u128)P_HI << 64) | P_LO;
-  const u128 d = A - B;
-  const u128 r = A < B ? d + P : d;
-  return fe{(uint64_t)r, (uint64_t)(r >> 64)};
-}
-#else
 // a + b mod p (inputs canonical), branch-free: with s = a + b mod 2^128, the result is
 // s + C (mod 2^128) exactly when a + b >= p, i.e. when either addition carries out.
 __host__ __device__ inline fe fe_add(fe a, fe b) {
@@ -64,7 +44,6 @@ __host__ __device__ inline fe fe_sub(fe a, fe b) {
   return b1 ? fe{tlo, thi} : fe{lo, hi};
 }
 
-#endif
 
 // Branching forms: cheaper when operands are small (the constraint evaluator's selectors
 // and flags rarely wrap, so whole wavefronts skip the reduction).

@@ -790,6 +790,9 @@ struct Acc {
   __device__ __forceinline__ void emit(fe v) { mul_acc(al[ix++], v, a); }
 };
 
+// POSE: the PoseidonAir block is compiled into a separate instance so that VM-only segments
+// keep the smaller register footprint
+template <bool POSE>
 __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restrict__ lde, const fe* __restrict__ roots,
                                                               int roots_shift, const fe* __restrict__ pertab,
                                                               const fe* __restrict__ bm,
@@ -826,6 +829,48 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
   A.ix = 0;
   A.al = K->alpha;
   const fe one = fe_one();
+
+  if (POSE) {
+    // ---------------- PoseidonAir (poseidon.rs:65-162): y = MDS s^3 (+ rc_j) is the same
+    // for all 27 rounds but the round constant, so it is formed once per point
+    const fe pa = cur(C.pose_active);
+    fe s3[12];
+#pragma unroll
+    for (int i = 0; i < 12; i++) s3[i] = fe_cube(cur(C.lanes_start + i));
+    fe ms[12];
+    for (int i = 0; i < 12; i++) {
+      uint32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < 12; k++) mul_acc(c_air.pose_mds[i][k], s3[k], acc);
+      ms[i] = reduce288(acc);
+    }
+    for (int j = 0; j < 27; j++) {
+      const fe g = fe_mul(pa, per[1 + j]);
+      for (int i = 0; i < 12; i++)
+        A.emit(fe_mul(g, fe_sub(nxt(C.lanes_start + i), fe_add(ms[i], c_air.pose_rc[j][i]))));
+    }
+    const fe g_hold = fe_sub_sel(p_pad, p_pad_last);
+    for (int i = 0; i < 12; i++) A.emit(fe_mul(g_hold, fe_sub(nxt(C.lanes_start + i), cur(C.lanes_start + i))));
+    if (c_air.pose_bind) {
+      const fe gate = fe_mul(fe_mul(p_map, pa), cur(C.op[8]));
+      fe rr[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) rr[i] = cur(C.r_start + i);
+      for (int lane = 0; lane < 10; lane++) {
+        const fe b0 = cur(C.sel_s_bits + lane * 3), b1 = cur(C.sel_s_bits + lane * 3 + 1),
+                 b2 = cur(C.sel_s_bits + lane * 3 + 2), act = cur(C.sel_s_active + lane);
+        const fe nb0 = fe_sub_sel(one, b0), nb1 = fe_sub_sel(one, b1), nb2 = fe_sub_sel(one, b2);
+        const fe s0 = fe_add(fe_mul(b0, rr[1]), fe_mul(nb0, rr[0]));
+        const fe s1 = fe_add(fe_mul(b0, rr[3]), fe_mul(nb0, rr[2]));
+        const fe s2 = fe_add(fe_mul(b0, rr[5]), fe_mul(nb0, rr[4]));
+        const fe s3v = fe_add(fe_mul(b0, rr[7]), fe_mul(nb0, rr[6]));
+        const fe t0 = fe_add(fe_mul(b1, s1), fe_mul(nb1, s0));
+        const fe t1 = fe_add(fe_mul(b1, s3v), fe_mul(nb1, s2));
+        const fe sel_val = fe_add(fe_mul(b2, t1), fe_mul(nb2, t0));
+        A.emit(fe_mul(gate, fe_sub(cur(C.lanes_start + lane), fe_mul(act, sel_val))));
+      }
+    }
+  }
 
   if (c_air.feat_vm) {
     // ---------------- VmCtrlAir (ctrl.rs:114-390)
@@ -1020,11 +1065,15 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
 }
 
 void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab, const fe* d_bm,
-                            const CeParams& p, ProofConsts* dK, fe* d_out, hipStream_t s) {
+                            const CeParams& p, ProofConsts* dK, bool pose_block, fe* d_out, hipStream_t s) {
   (void)hipMemcpyAsync(&dK->ce, &p, sizeof p, hipMemcpyHostToDevice, s);
   int shift = ilog2s(Ntab) - ilog2s(p.ce);
-  constraint_eval_kernel<<<(unsigned)((p.ce + 255) / 256), 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK,
-                                                                         d_out);
+  if (pose_block)
+    constraint_eval_kernel<true><<<(unsigned)((p.ce + 255) / 256), 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm,
+                                                                                 dK, d_out);
+  else
+    constraint_eval_kernel<false><<<(unsigned)((p.ce + 255) / 256), 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm,
+                                                                                  dK, d_out);
 }
 
 __global__ void boundary_scatter_kernel(const uint32_t* slot, const uint32_t* step, const fe* beta, size_t na, size_t n,

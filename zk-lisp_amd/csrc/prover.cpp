@@ -419,7 +419,8 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->ce.ensure(ce * sizeof(fe));
   {
     KScope k(C, KF_CEVAL);
-    launch_constraint_eval(C->lde.f(), roots, Ntab, C->pertab.f(), C->bm.f(), cp, dK, C->ce.f(), s);
+    launch_constraint_eval(C->lde.f(), roots, Ntab, C->pertab.f(), C->bm.f(), cp, dK, air.dev.pose_block != 0,
+                           C->ce.f(), s);
   }
   T.mark(3);
 

@@ -3,7 +3,9 @@
 // vm/trace/rom.rs:29-108) with the {vm, rom} segment layout (vm/trace/mod.rs:80-235),
 // plus the AIR public inputs prove_segment derives (prove.rs:292-423, 1197-1392).
 // Program: (levels-1) ALU ops cycling Const/Add/Mov/Mul over r0..r7, splitmix64 choices,
-// immediates < 2^63, then End.  This is input preparation, not the measured path.
+// immediates < 2^63, then End.  flags bit 0 interleaves SAbsorbN / SSqueeze sponge ops
+// (vm/trace/vm.rs:565-672, vm/trace/poseidon.rs:9-87) so the Poseidon AIR block
+// (poseidon.rs:26-162) is exercised.  This is input preparation, not the measured path.
 #include <stdio.h>
 #include <string.h>
 
@@ -23,8 +25,8 @@ uint64_t splitmix(uint64_t& s) {
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
-enum Kind { K_CONST = 0, K_MOV = 1, K_ADD = 2, K_SUB = 3, K_MUL = 4, K_END = 99 };
-struct Op { Kind k; int dst, a, b; uint64_t imm; };
+enum Kind { K_CONST = 0, K_MOV = 1, K_ADD = 2, K_SUB = 3, K_MUL = 4, K_ABSORB = 10, K_SQUEEZE = 11, K_END = 99 };
+struct Op { Kind k; int dst, a, b; uint64_t imm; int nabs; int abs_regs[3]; };
 
 struct Table {
   zkl_f128* t;
@@ -35,11 +37,52 @@ struct Table {
     for (int i = 0; i < 8; i++) set(start + i, row, fe_zero());
     set(start + idx, row, fe_one());
   }
+  // sponge lane selectors: lane j < k reads register regs[j] (3 index bits + active flag)
+  void sponge_sel(const Layout& L, size_t row, const int* regs, int k) {
+    for (int lane = 0; lane < 10; lane++) {
+      bool on = lane < k;
+      int idx = on ? regs[lane] : 0;
+      for (int bit = 0; bit < 3; bit++) set(L.sel_s_bits + lane * 3 + bit, row, on ? fe{(uint64_t)((idx >> bit) & 1), 0} : fe_zero());
+      set(L.sel_s_active + lane, row, on ? fe_one() : fe_zero());
+    }
+  }
 };
+
+// One level's Poseidon lanes (vm/trace/poseidon.rs:9-87): map row = [inputs (zero padded
+// to 10), dom0, dom1]; round row 1+j = state before round j; final and pad rows = output.
+void level_absorb(Table& T, const Layout& L, const PoseidonSuite& ps, size_t level, const fe* in, int nin) {
+  size_t b = level * 32;
+  fe st[12];
+  for (int i = 0; i < 12; i++) st[i] = fe_zero();
+  for (int i = 0; i < nin && i < 10; i++) st[i] = in[i];
+  st[10] = ps.dom[0];
+  st[11] = ps.dom[1];
+  for (int i = 0; i < 12; i++) T.set(L.lanes_start + i, b, st[i]);
+  for (int j = 0; j < 27; j++) {
+    for (int i = 0; i < 12; i++) T.set(L.lanes_start + i, b + 1 + j, st[i]);
+    fe s3[12], y[12];
+    for (int i = 0; i < 12; i++) s3[i] = fe_cube(st[i]);
+    for (int i = 0; i < 12; i++) {
+      fe acc = fe_zero();
+      for (int k = 0; k < 12; k++) acc = fe_add(acc, fe_mul(ps.mds[i][k], s3[k]));
+      y[i] = fe_add(acc, ps.rc[j][i]);
+    }
+    memcpy(st, y, sizeof st);
+  }
+  for (size_t r = b + 28; r < b + 32; r++)
+    for (int i = 0; i < 12; i++) T.set(L.lanes_start + i, r, st[i]);
+}
 }  // namespace
 
 extern "C" int zkl_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128* trace, zkl_air_public_inputs* pi,
                                     uint32_t* width_out) {
+  return zkl_synth_vm_segment_ex(seed, log_n, 0, trace, pi, width_out);
+}
+
+extern "C" int zkl_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f128* trace,
+                                       zkl_air_public_inputs* pi, uint32_t* width_out) {
+  if (flags & ~1u) return ZKL_E_INVALID;
+  const bool sponge = flags & 1;
   if (log_n < 5 || log_n > 26) return ZKL_E_INVALID;
   const Layout L = make_layout(true, false, false, false, true);
   if (width_out) *width_out = (uint32_t)L.width;
@@ -51,8 +94,8 @@ extern "C" int zkl_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128* tra
   Table T{trace, n};
 
   char desc[128];
-  snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 seed=0x%016llx levels=%zu", (unsigned long long)seed,
-           levels);
+  snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 %sseed=0x%016llx levels=%zu", sponge ? "sponge " : "",
+           (unsigned long long)seed, levels);
   uint8_t pid[32];
   blake3_hash((const uint8_t*)desc, strlen(desc), pid);
   PoseidonSuite ps = derive_poseidon_suite(pid, 27);
@@ -61,14 +104,22 @@ extern "C" int zkl_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128* tra
   {
     uint64_t st = seed;
     const Kind cyc[4] = {K_CONST, K_ADD, K_MOV, K_MUL};
+    // every 8 levels: absorb, const, absorb, squeeze, add, mov, mul, squeeze-with-nothing-pending
+    const Kind cyc_s[8] = {K_ABSORB, K_CONST, K_ABSORB, K_SQUEEZE, K_ADD, K_MOV, K_MUL, K_SQUEEZE};
     for (size_t l = 0; l + 1 < levels; l++) {
       uint64_t r = splitmix(st);
       Op& o = ops[l];
-      o.k = cyc[l % 4];
+      o = Op{};
+      o.k = sponge ? cyc_s[l % 8] : cyc[l % 4];
       o.dst = (int)(r & 7); o.a = (int)((r >> 3) & 7); o.b = (int)((r >> 6) & 7);
       o.imm = o.k == K_CONST ? (splitmix(st) >> 1) : 0;
+      if (o.k == K_ABSORB) {
+        o.nabs = 1 + (int)((r >> 9) % 3);
+        for (int i = 0; i < 3; i++) o.abs_regs[i] = (int)((r >> (12 + 3 * i)) & 7);
+      }
     }
-    ops[levels - 1] = Op{K_END, 0, 0, 0, 0};
+    ops[levels - 1] = Op{};
+    ops[levels - 1].k = K_END;
   }
   // schedule gates, pc, domain tags (mod.rs:386-470)
   for (size_t l = 0; l < levels; l++) {
@@ -82,13 +133,35 @@ extern "C" int zkl_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128* tra
   }
   // VmTraceBuilder
   fe regs[8] = {};
+  int pending[10], npending = 0;
   for (size_t l = 0; l < levels; l++) {
     fe next[8];
     memcpy(next, regs, sizeof next);
     size_t b = l * 32, rm = b, rf = b + 28;
     if (l == 0) T.set(L.pi_prog, 0, be_from_le16(pid));
     const Op& o = ops[l];
-    if (o.k != K_END) {
+    if (o.k == K_ABSORB || o.k == K_SQUEEZE) {  // SAbsorbN / SSqueeze (vm.rs:565-672)
+      T.set(L.rom_op_start + 8, rm, fe_one());
+      int sel_regs[10], k = 0;
+      if (o.k == K_ABSORB) {
+        for (int i = 0; i < o.nabs; i++) { sel_regs[k++] = o.abs_regs[i]; pending[npending++] = o.abs_regs[i]; }
+      } else {
+        for (int i = 0; i < npending; i++) sel_regs[k++] = pending[i];
+      }
+      for (size_t row : {rm, rf}) {
+        T.set(L.op[8], row, fe_one());
+        T.sponge_sel(L, row, sel_regs, k);
+      }
+      if (o.k == K_SQUEEZE) {
+        T.sel(rf, L.sel_dst0, o.dst);
+        fe in[10];
+        for (int i = 0; i < k; i++) in[i] = regs[sel_regs[i]];
+        level_absorb(T, L, ps, l, in, k);
+        next[o.dst] = T.get(L.lanes_start, rf);
+        npending = 0;
+        for (size_t r = b; r < b + 32; r++) T.set(L.pose_active, r, fe_one());
+      }
+    } else if (o.k != K_END) {
       int oh = (int)o.k;
       T.set(L.rom_op_start + oh, rm, fe_one());
       for (size_t row : {rm, rf}) {
@@ -151,8 +224,8 @@ extern "C" int zkl_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128* tra
   // AIR public inputs for the whole-trace segment
   memcpy(pi->program_id, pid, 32);
   memcpy(pi->program_commitment, pid, 32);
-  pi->feature_mask = 2;  // FM_VM
-  pi->segment_feature_mask = 2;
+  pi->feature_mask = sponge ? (2 | 32 | 1) : 2;  // FM_VM (+ FM_SPONGE | FM_POSEIDON)
+  pi->segment_feature_mask = pi->feature_mask;
   pi->vm_out_reg = 0;
   pi->vm_out_row = 29;
   for (size_t l = levels; l-- > 0;) {  // vm_output_from_trace_with_layout (utils.rs:262-289)

@@ -106,6 +106,8 @@ def load_library():
     lib.zkl_hip_synchronize.argtypes = [C.c_void_p]
     lib.zkl_select_partitions.argtypes = [C.c_uint32, C.c_uint32, P(C.c_uint32), P(C.c_uint32)]
     lib.zkl_synth_vm_segment.argtypes = [C.c_uint64, C.c_uint32, C.c_void_p, P(AirPublicInputs), P(C.c_uint32)]
+    lib.zkl_synth_vm_segment_ex.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p, P(AirPublicInputs),
+                                            P(C.c_uint32)]
     lib.zkl_hip_ntt.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int]
     lib.zkl_hip_hash_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]
     lib.zkl_hip_merkle_tree.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
@@ -135,15 +137,16 @@ def proof_options(width, length, queries=64, blowup=16, grind=16) -> ProofOption
     return ProofOptions(queries, blowup, grind, 1, 2, 1, 0, 0, parts, rate)
 
 
-def synth_vm_segment(seed: int, log_n: int):
-    """Synthetic VM segment (workload generator): returns (trace, pi, width), trace column-major."""
+def synth_vm_segment(seed: int, log_n: int, flags: int = 0):
+    """Synthetic VM segment (workload generator): returns (trace, pi, width), trace column-major.
+    flags bit 0 adds sponge ops (FM_SPONGE | FM_POSEIDON segments)."""
     lib = load_library()
     w = C.c_uint32()
-    lib.zkl_synth_vm_segment(seed, log_n, None, None, C.byref(w))
+    lib.zkl_synth_vm_segment_ex(seed, log_n, flags, None, None, C.byref(w))
     n = 1 << log_n
     trace = (F128 * (w.value * n))()
     pi = AirPublicInputs()
-    rc = lib.zkl_synth_vm_segment(seed, log_n, C.cast(trace, C.c_void_p), C.byref(pi), C.byref(w))
+    rc = lib.zkl_synth_vm_segment_ex(seed, log_n, flags, C.cast(trace, C.c_void_p), C.byref(pi), C.byref(w))
     if rc != 0:
         raise ZklError(rc, "synth_vm_segment failed")
     return trace, pi, w.value
