@@ -170,9 +170,18 @@ int zkl_hip_ntt(zkl_ctx* ctx, void* d_data, uint32_t n_cols, uint32_t n, int dif
  * column-major trace (204 x 2^log_n) and the AIR public inputs. */
 int zkl_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128* trace_out,
                          zkl_air_public_inputs* pi_out, uint32_t* width_out);
-/* Same with flags: bit 0 interleaves SAbsorbN / SSqueeze sponge ops (vm/trace/vm.rs:565-672)
- * so the segment enables FM_VM | FM_SPONGE | FM_POSEIDON and the Poseidon AIR block
- * (zk-lisp-proof-winterfell/src/air/poseidon.rs:26-162).  flags = 0 is zkl_synth_vm_segment. */
+/* Same with program flags (flags = 0 is zkl_synth_vm_segment); the trace is built in the
+ * segment layout the features imply ({vm, rom} 204, {vm, ram, rom} 212, {vm, merkle, rom} 211,
+ * all 219, vm/layout.rs:183-313):
+ *   ZKL_SYN_SPONGE  SAbsorbN / SSqueeze ops (vm/trace/vm.rs:565-672): FM_SPONGE | FM_POSEIDON,
+ *                   PoseidonAir block (vm/air/poseidon.rs:26-162)
+ *   ZKL_SYN_RAM     Load / Store over 8 addresses (vm.rs:803-842): FM_RAM, RamAir block
+ *                   (vm/air/ram.rs:26-236) incl. the delta_clk range gadget
+ *   ZKL_SYN_MERKLE  one MerkleStepFirst/Step/Last path (vm.rs:675-800): FM_MERKLE | FM_POSEIDON,
+ *                   MerkleAir block (vm/air/merkle.rs:26-134); needs log_n >= 8 */
+#define ZKL_SYN_SPONGE 1u
+#define ZKL_SYN_RAM 2u
+#define ZKL_SYN_MERKLE 4u
 int zkl_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f128* trace_out,
                             zkl_air_public_inputs* pi_out, uint32_t* width_out);
 

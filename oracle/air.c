@@ -22,14 +22,8 @@
 
 #define NR 8
 #define STEPS 32
-#define FM_POSEIDON 1ull
-#define FM_VM 2ull
-#define FM_VM_EXPECT 16ull
-#define FM_SPONGE 32ull
-#define FM_MERKLE 64ull
-#define FM_RAM 128ull
 
-enum { U_ASSERT = 0, U_ASSERT_BIT, U_ASSERT_RANGE, U_DIVMOD, U_MULWIDE, U_DIV128, U_EQ, U_SPONGE };
+enum { U_ASSERT = 0, U_ASSERT_BIT, U_ASSERT_RANGE, U_DIVMOD, U_MULWIDE, U_DIV128, U_EQ, U_SPONGE, U_RAM_DCLK };
 
 void cols_for_config(int vm, int ram, int sponge, int merkle, int rom, zk_cols *c) {
   (void)vm; (void)sponge;
@@ -48,7 +42,11 @@ void cols_for_config(int vm, int ram, int sponge, int merkle, int rom, zk_cols *
   cur += 40;
   c->imm = cur; c->eq_inv = cur + 1;
   cur += 2;
+  c->ram_sorted = cur; c->ram_s_addr = cur + 1; c->ram_s_clk = cur + 2; c->ram_s_val = cur + 3;
+  c->ram_s_is_write = cur + 4; c->ram_s_last_write = cur + 5; c->ram_gp_unsorted = cur + 6; c->ram_gp_sorted = cur + 7;
   if (ram) cur += 8;
+  c->merkle_g = cur; c->merkle_dir = cur + 1; c->merkle_sib = cur + 2; c->merkle_acc = cur + 3;
+  c->merkle_first = cur + 4; c->merkle_last = cur + 5; c->merkle_leaf = cur + 6;
   if (merkle) cur += 7;
   c->pi_prog = cur++;
   c->pc = cur++;
@@ -119,12 +117,12 @@ int air_new(zk_air *air, const zkl_air_public_inputs *pi, uint32_t width, size_t
   air->feat_sponge = !!(eff & FM_SPONGE);
   air->feat_merkle = !!(eff & FM_MERKLE);
   air->feat_ram = !!(eff & FM_RAM);
-  if (air->feat_merkle || air->feat_ram) return -1;
   int pid_nz = 0, com_nz = 0;
   for (int i = 0; i < 32; i++) { pid_nz |= pi->program_id[i]; com_nz |= pi->program_commitment[i]; }
   air->rom_enabled = pid_nz != 0;
   air->commit_nonzero = com_nz != 0;
   air->vm_usage_mask = pi->vm_usage_mask;
+  air->ram_delta_clk_bits = pi->ram_delta_clk_bits;
   air->trace_len = n;
   zk_cols base;
   cols_for_config(1, 1, 1, 1, 1, &base);
@@ -145,56 +143,76 @@ int air_new(zk_air *air, const zkl_air_public_inputs *pi, uint32_t width, size_t
   rom_w(1037, air->rom_w1);
   if (pid_nz) program_field_commitment(pi->program_id, air->program_fe);
 
-  /* degrees in module order (mod.rs:217-238) */
+  air->merkle_root = be_from_le8(pi->merkle_root);
+  /* degrees in module order (mod.rs:217-238); DEG(base, has the 32-cycle) */
   int nd = 0;
+#define DEG(b, cyc) do { air->deg_base[nd] = (b); air->deg_cyc[nd] = (cyc); nd++; } while (0)
   uint32_t m = pi->vm_usage_mask;
   if (air->feat_poseidon) { /* PoseidonAir::push_degrees (poseidon.rs:26-62) */
-    for (int i = 0; i < POS_ROUNDS * 12; i++) air->deg_base[nd++] = 4;
-    for (int i = 0; i < 12; i++) air->deg_base[nd++] = 1;
+    for (int i = 0; i < POS_ROUNDS * 12; i++) DEG(4, 1);
+    for (int i = 0; i < 12; i++) DEG(1, 1);
     air->pose_bind = air->feat_vm && air->feat_sponge && (m & (1u << U_SPONGE));
     if (air->pose_bind) {
       static const int lane_bases[10] = {6, 6, 3, 3, 3, 3, 3, 3, 3, 3};
-      for (int i = 0; i < 10; i++) air->deg_base[nd++] = lane_bases[i];
+      for (int i = 0; i < 10; i++) DEG(lane_bases[i], 1);
     }
   }
   if (air->feat_vm) {
-    for (int i = 0; i < 5 * NR; i++) air->deg_base[nd++] = 2;
-    for (int i = 0; i < 5; i++) air->deg_base[nd++] = 1;
-    for (int i = 0; i < NR; i++) air->deg_base[nd++] = 2;
+    for (int i = 0; i < 5 * NR; i++) DEG(2, 1);
+    for (int i = 0; i < 5; i++) DEG(1, 1);
+    for (int i = 0; i < NR; i++) DEG(2, 1);
     if (air->feat_sponge && (m & (1u << U_SPONGE)))
-      for (int i = 0; i < 40; i++) air->deg_base[nd++] = 2;
-    air->deg_base[nd++] = 2;
-    for (int i = 0; i < 17; i++) air->deg_base[nd++] = 2;
-    air->deg_base[nd++] = 2;
-    for (int i = 0; i < 17; i++) air->deg_base[nd++] = 2;
-    air->deg_base[nd++] = 1;
-    air->deg_base[nd++] = 1;
+      for (int i = 0; i < 40; i++) DEG(2, 1);
+    DEG(2, 1);
+    for (int i = 0; i < 17; i++) DEG(2, 1);
+    DEG(2, 1);
+    for (int i = 0; i < 17; i++) DEG(2, 1);
+    DEG(1, 1);
+    DEG(1, 1);
     /* ALU */
-    for (int i = 0; i < NR; i++) air->deg_base[nd++] = 1;
-    for (int i = 0; i < NR; i++) air->deg_base[nd++] = 7;
-    if (m & (1u << U_EQ)) for (int i = 0; i < 2; i++) air->deg_base[nd++] = 5;
-    if (m & (1u << U_DIVMOD)) for (int i = 0; i < 2; i++) air->deg_base[nd++] = 5;
-    if (m & (1u << U_ASSERT)) air->deg_base[nd++] = 5;
-    if (m & (1u << U_ASSERT_BIT)) air->deg_base[nd++] = 5;
-    if (m & (1u << U_ASSERT_RANGE)) for (int i = 0; i < 33; i++) air->deg_base[nd++] = 5;
-    if (m & (1u << U_MULWIDE)) air->deg_base[nd++] = 5;
-    if (m & (1u << U_DIV128)) for (int i = 0; i < 2; i++) air->deg_base[nd++] = 5;
+    for (int i = 0; i < NR; i++) DEG(1, 1);
+    for (int i = 0; i < NR; i++) DEG(7, 1);
+    if (m & (1u << U_EQ)) for (int i = 0; i < 2; i++) DEG(5, 1);
+    if (m & (1u << U_DIVMOD)) for (int i = 0; i < 2; i++) DEG(5, 1);
+    if (m & (1u << U_ASSERT)) DEG(5, 1);
+    if (m & (1u << U_ASSERT_BIT)) DEG(5, 1);
+    if (m & (1u << U_ASSERT_RANGE)) for (int i = 0; i < 33; i++) DEG(5, 1);
+    if (m & (1u << U_MULWIDE)) DEG(5, 1);
+    if (m & (1u << U_DIV128)) for (int i = 0; i < 2; i++) DEG(5, 1);
+  }
+  if (air->feat_ram) { /* RamAir::push_degrees (ram.rs:26-79) */
+    DEG(4, 1);
+    DEG(2, 0); DEG(5, 0); DEG(3, 0); DEG(6, 0); DEG(5, 0);
+    if (m & (1u << U_RAM_DCLK)) {
+      for (int i = 0; i < 32; i++) if ((pi->ram_delta_clk_bits >> i) & 1) DEG(5, 0);
+      DEG(5, 0);
+    }
+    DEG(2, 0);
+  }
+  if (air->feat_merkle) { /* MerkleAir::push_degrees (merkle.rs:26-58) */
+    DEG(3, 1); DEG(3, 1); DEG(3, 1); DEG(2, 1); DEG(3, 1); DEG(3, 1); DEG(3, 1);
   }
   if (air->rom_enabled) {
-    for (int i = 0; i < 81; i++) air->deg_base[nd++] = 3;
-    for (int i = 0; i < 3; i++) air->deg_base[nd++] = 1;
-    for (int i = 0; i < 2; i++) air->deg_base[nd++] = 1;
+    for (int i = 0; i < 81; i++) DEG(3, 1);
+    for (int i = 0; i < 3; i++) DEG(1, 1);
+    for (int i = 0; i < 2; i++) DEG(1, 1);
   }
   if (nd == 0) return -3; /* AIR with no constraints: not a VM segment */
   air->n_tc = nd;
 
-  /* AirContext: ce_blowup = max next_pow2(base + cycles - 1) (min 2); all constraints carry
-   * one cycle of length 32; num composition columns = ceil((max_eval - (n-1)) / n) */
-  int maxb = 0;
-  for (int i = 0; i < nd; i++) if (air->deg_base[i] > maxb) maxb = air->deg_base[i];
-  int ceb = 1; while (ceb < maxb) ceb <<= 1; if (ceb < 2) ceb = 2;
+#undef DEG
+  /* AirContext: ce_blowup = max next_pow2(base + cycles - 1) (min 2); eval degree =
+   * base (n-1) + cycles (n/32) 31; num composition columns = ceil((max_eval - (n-1)) / n) */
+  int ceb = 2;
+  size_t max_eval = 0;
+  for (int i = 0; i < nd; i++) {
+    int need = 1;
+    while (need < air->deg_base[i] + air->deg_cyc[i] - 1) need <<= 1;
+    if (need > ceb) ceb = need;
+    size_t ev = (size_t)air->deg_base[i] * (n - 1) + (air->deg_cyc[i] ? (n / STEPS) * (STEPS - 1) : 0);
+    if (ev > max_eval) max_eval = ev;
+  }
   air->ce_blowup = ceb;
-  size_t max_eval = (size_t)maxb * (n - 1) + (n / STEPS) * (STEPS - 1);
   air->n_comp_cols = (int)((max_eval - (n - 1) + n - 1) / n);
 
   /* ---- assertions ---- */
@@ -488,6 +506,71 @@ void air_eval_transition(const zk_air *air, const fe *cur, const fe *nxt, const 
       fe eqt = fe_mul(imm, fe_add(fe_mul(mode64, eq64), fe_mul(fe_sub(1, mode64), eq32)));
       res[ix++] = fe_add(fe_mul(p_final, fe_mul(bo[ARANGE], eqt)), s_eq);
     }
+  }
+
+  if (air->feat_ram) {
+    /* ---------------- RamAir (ram.rs:82-236) ---------------- */
+    fe p_pad_ = per[29];
+    fe g_hold = fe_sub(p_pad_, p_pad_last);
+    fe op_load = cur[c->op[15]], op_store = cur[c->op[16]];
+    fe event = fe_mul(p_final, fe_add(op_load, op_store));
+    fe q0 = air->program_fe[0], q2 = fe_sqr(q0), q3 = fe_mul(q2, q0), q4 = fe_sqr(q2), q5 = fe_mul(q4, q0);
+    fe r1 = fe_add(q2, 1), r2 = fe_add(q3, q0), r3 = fe_add(q5, 7);
+    fe a_ev = 0, b_ev = 0;
+    for (int i = 0; i < NR; i++) {
+      fe ri = cur[c->r_start + i];
+      a_ev = fe_add(a_ev, fe_mul(cur[c->sel_a + i], ri));
+      b_ev = fe_add(b_ev, fe_mul(cur[c->sel_b + i], ri));
+    }
+    fe w_ev = op_store;
+    fe val_ev = fe_add(fe_mul(w_ev, b_ev), fe_mul(fe_sub(1, w_ev), cur[c->imm]));
+    fe comp_uns = fe_add(fe_add(fe_add(a_ev, fe_mul(r1, cur[c->pc])), fe_mul(r2, val_ev)), fe_mul(r3, w_ev));
+    fe gu = cur[c->ram_gp_unsorted], gu_n = nxt[c->ram_gp_unsorted];
+    res[ix++] = fe_add(fe_add(fe_mul(event, fe_sub(gu_n, fe_add(gu, comp_uns))), fe_mul(fe_sub(1, event), fe_sub(gu_n, gu))),
+                       fe_mul(g_hold, fe_sub(gu_n, gu)));
+    fe s_on = cur[c->ram_sorted], s_addr = cur[c->ram_s_addr], s_clk = cur[c->ram_s_clk], s_val = cur[c->ram_s_val],
+       s_w = cur[c->ram_s_is_write], lastw = cur[c->ram_s_last_write];
+    fe d_addr = fe_sub(nxt[c->ram_s_addr], s_addr);
+    fe same = fe_sub(1, fe_mul(d_addr, cur[c->eq_inv]));
+    fe comp = fe_add(fe_add(fe_add(s_addr, fe_mul(r1, s_clk)), fe_mul(r2, s_val)), fe_mul(r3, s_w));
+    fe gs = cur[c->ram_gp_sorted], gs_n = nxt[c->ram_gp_sorted];
+    res[ix++] = fe_add(fe_mul(s_on, fe_sub(gs_n, fe_add(gs, comp))), fe_mul(fe_sub(1, s_on), fe_sub(gs_n, gs)));
+    fe sw_val = fe_mul(s_w, s_val);
+    fe keep = fe_add(fe_mul(same, fe_add(fe_mul(fe_sub(1, s_w), lastw), sw_val)), fe_mul(fe_sub(1, same), sw_val));
+    res[ix++] = fe_mul(s_on, fe_sub(nxt[c->ram_s_last_write], keep));
+    res[ix++] = fe_mul(fe_mul(s_on, fe_sub(1, s_w)), fe_sub(s_val, lastw));
+    fe s_on_n = nxt[c->ram_sorted];
+    res[ix++] = fe_mul(fe_mul(fe_mul(fe_mul(s_on, s_on_n), fe_sub(1, same)), fe_sub(1, nxt[c->ram_s_is_write])),
+                       nxt[c->ram_s_val]);
+    res[ix++] = fe_mul(s_on, fe_mul(same, fe_sub(same, 1)));
+    if (m & (1u << U_RAM_DCLK)) {
+      fe d_clk = fe_sub(nxt[c->ram_s_clk], s_clk);
+      fe sum = 0, pow2 = 1;
+      fe g_same = fe_mul(s_on, same);
+      for (int i = 0; i < 32; i++) {
+        fe bi = cur[c->gadget_b + i];
+        if ((air->ram_delta_clk_bits >> i) & 1) res[ix++] = fe_mul(g_same, fe_mul(bi, fe_sub(bi, 1)));
+        sum = fe_add(sum, fe_mul(pow2, bi));
+        pow2 = fe_add(pow2, pow2);
+      }
+      res[ix++] = fe_mul(fe_mul(fe_mul(s_on, s_on_n), same), fe_sub(d_clk, sum));
+    }
+    res[ix++] = fe_mul(p_last, fe_sub(gu, gs));
+  }
+
+  if (air->feat_merkle) {
+    /* ---------------- MerkleAir (merkle.rs:60-134) ---------------- */
+    fe g = cur[c->merkle_g], dir = cur[c->merkle_dir], acc = cur[c->merkle_acc], sib = cur[c->merkle_sib];
+    fe pg = fe_mul(p_map, g);
+    res[ix++] = fe_mul(pg, fe_mul(dir, fe_sub(dir, 1)));
+    fe left = fe_add(fe_mul(fe_sub(1, dir), acc), fe_mul(dir, sib));
+    fe right = fe_add(fe_mul(fe_sub(1, dir), sib), fe_mul(dir, acc));
+    res[ix++] = fe_mul(pg, fe_sub(cur[c->lanes_start], left));
+    res[ix++] = fe_mul(pg, fe_sub(cur[c->lanes_start + 1], right));
+    res[ix++] = fe_mul(fe_mul(g, g_carry), fe_sub(nxt[c->merkle_acc], acc));
+    res[ix++] = fe_mul(fe_mul(pg, cur[c->merkle_first]), fe_sub(acc, cur[c->merkle_leaf]));
+    res[ix++] = fe_mul(fe_mul(fe_mul(p_final, g), cur[c->merkle_last]), fe_sub(acc, air->merkle_root));
+    res[ix++] = fe_mul(fe_mul(fe_mul(p_pad_last, g), nxt[c->merkle_g]), fe_sub(nxt[c->merkle_acc], acc));
   }
 
   /* ---------------- RomAir (rom.rs:57-120); runs when program_commitment != 0 ------- */

@@ -60,12 +60,23 @@ void coset_evaluate(const fe *coeffs, size_t ncoef, fe *out, size_t n, fe offset
 fe poly_eval(const fe *c, size_t n, fe x);
 
 /* ---------------- AIR (vm/air/ (all modules), vm/layout.rs) ---------------- */
+/* feature bits (zk-lisp-proof/src/pi.rs:23-28) */
+#define FM_POSEIDON 1ull
+#define FM_VM 2ull
+#define FM_VM_EXPECT 16ull
+#define FM_SPONGE 32ull
+#define FM_MERKLE 64ull
+#define FM_RAM 128ull
+
 typedef struct {
   int lanes_start, g_map, g_final, g_r_start, mask, r_start;
   int op[17];         /* const, mov, add, sub, mul, neg, eq, select, sponge, assert, assert_bit,
                          assert_range, divmod, div128, mulwide, load, store */
   int sel_dst0, sel_a, sel_b, sel_c, sel_dst1, sel_s_bits, sel_s_active, imm, eq_inv;
   int pi_prog, pc, rom_op_start, pose_active, gadget_b, rom_s;
+  int ram_sorted, ram_s_addr, ram_s_clk, ram_s_val, ram_s_is_write, ram_s_last_write, ram_gp_unsorted,
+      ram_gp_sorted;                                       /* layout.rs:247-256 */
+  int merkle_g, merkle_dir, merkle_sib, merkle_acc, merkle_first, merkle_last, merkle_leaf; /* :262-270 */
   int width;
 } zk_cols;
 void cols_for_config(int vm, int ram, int sponge, int merkle, int rom, zk_cols *c);
@@ -74,7 +85,7 @@ void cols_for_config(int vm, int ram, int sponge, int merkle, int rom, zk_cols *
 typedef struct {
   zk_cols cols;
   int feat_poseidon, feat_vm, feat_vm_expect, feat_sponge, feat_merkle, feat_ram, rom_enabled;
-  uint32_t vm_usage_mask;
+  uint32_t vm_usage_mask, ram_delta_clk_bits;
   int commit_nonzero;
   fe rom_rc[POS_ROUNDS][3], rom_mds[3][3];
   fe rom_w0[59], rom_w1[59];
@@ -82,9 +93,11 @@ typedef struct {
   fe pose_mds[12][12], pose_rc[POS_ROUNDS][12]; /* AIR Poseidon suite (suite_id = program_id) */
   int pose_bind;                                 /* VM->lane bindings present (poseidon.rs:48-62) */
   fe program_fe[2];
+  fe merkle_root;                                /* be_from_le8(pi.merkle_root) (merkle.rs:118) */
   /* transition constraint degrees (base, has_cycle32) */
   int n_tc;
   int deg_base[MAX_TC];
+  unsigned char deg_cyc[MAX_TC];
   /* assertions sorted (step, column) after dedup */
   size_t n_assert;
   uint32_t *as_col, *as_step;

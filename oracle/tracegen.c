@@ -3,10 +3,14 @@
  *
  * Synthetic VM segment built the way the reference builds traces:
  *   vm/trace/mod.rs:386-524     build_empty_trace / build_full_trace (schedule gates, pc, dom tags)
- *   vm/trace/vm.rs:58-888       VmTraceBuilder::fill_table (Const/Mov/Add/Sub/Mul/Neg/End)
+ *   vm/trace/vm.rs:58-888       VmTraceBuilder::fill_table (Const/Mov/Add/Sub/Mul/Neg/SAbsorbN/SSqueeze/
+ *                               MerkleStepFirst/MerkleStep/MerkleStepLast/Load/Store/End)
+ *   vm/trace/poseidon.rs:9-87   apply_level_absorb
+ *   vm/trace/ram.rs:43-271      RamTraceBuilder (sorted table in pad rows, last-write, delta_clk bits,
+ *                               grand-product compressors)
  *   vm/trace/vm.rs:890-921      op_to_one_hot (ROM mirror)
  *   vm/trace/rom.rs:29-108      RomTraceBuilder (t=3 accumulator)
- *   vm/trace/mod.rs:80-235      SegmentLayout projection (we build the {vm,rom} layout directly)
+ *   vm/trace/mod.rs:80-235      SegmentLayout projection (we build the segment layout directly)
  *   prove.rs:292-423,1289-1392  AIR public inputs, vm_usage_mask
  *   utils.rs:262-289            vm_output_from_trace
  * Program: levels-1 ALU ops cycling Const/Add/Mov/Mul over r0..r7 (splitmix64 choices,
@@ -27,31 +31,64 @@ static uint64_t splitmix64(uint64_t *s) {
 }
 
 enum { OP_CONST = 0, OP_MOV = 1, OP_ADD = 2, OP_SUB = 3, OP_MUL = 4, OP_NEG = 5, OP_ABSORB = 10, OP_SQUEEZE = 11,
-       OP_END = 99 };
+       OP_CADDR = 12, OP_LOAD = 15, OP_STORE = 16, OP_MFIRST = 20, OP_MSTEP = 21, OP_MLAST = 22, OP_END = 99 };
 typedef struct { int kind; int dst, a, b; uint64_t imm; int nabs; int abs_regs[3]; } synth_op;
 
-/* flags bit 0: sponge program (SAbsorbN / SSqueeze, vm.rs:565-672) interleaved with ALU ops;
- * every 8 levels: absorb, const, absorb, squeeze, add, mov, mul, squeeze-with-nothing-pending */
+#define SYN_SPONGE 1u
+#define SYN_RAM 2u
+#define SYN_MERKLE 4u
+#define RAM_ADDR_REG 7
+
+/* Program generator.  flags 0: Const/Add/Mov/Mul cycle.  SYN_SPONGE: every 8 levels
+ * absorb, const, absorb, squeeze, add, mov, mul, squeeze-with-nothing-pending (vm.rs:565-672).
+ * SYN_RAM: 8-level block const-address (r7 <- 0..7), const, store, load, add, store, mul, load
+ * (vm.rs:803-842); ALU destinations avoid r7 so addresses repeat; stores, adds and muls
+ * read the latest result.  With both, the sponge block
+ * is followed by the RAM block.  SYN_MERKLE: levels 1..5 are bit r5, bit r6, MerkleStepFirst
+ * (leaf r0, dir r5, sib r1), MerkleStep (dir r6, sib r2), MerkleStepLast (dir r5, sib r3)
+ * (vm.rs:675-800), a single path whose root becomes pi.merkle_root. */
 static void synth_program(uint64_t seed, size_t levels, synth_op *ops, uint32_t flags) {
   uint64_t st = seed;
   static const int cyc[4] = {OP_CONST, OP_ADD, OP_MOV, OP_MUL};
   static const int cyc_s[8] = {OP_ABSORB, OP_CONST, OP_ABSORB, OP_SQUEEZE, OP_ADD, OP_MOV, OP_MUL, OP_SQUEEZE};
+  static const int cyc_r[8] = {OP_CADDR, OP_CONST, OP_STORE, OP_LOAD, OP_ADD, OP_STORE, OP_MUL, OP_LOAD};
+  int cycle[16], clen = 0;
+  if (flags & SYN_SPONGE) for (int i = 0; i < 8; i++) cycle[clen++] = cyc_s[i];
+  if (flags & SYN_RAM) for (int i = 0; i < 8; i++) cycle[clen++] = cyc_r[i];
+  if (!clen) for (int i = 0; i < 4; i++) cycle[clen++] = cyc[i];
+  int last_dst = 0;
   for (size_t l = 0; l + 1 < levels; l++) {
     uint64_t r = splitmix64(&st);
-    ops[l].kind = (flags & 1) ? cyc_s[l % 8] : cyc[l % 4];
-    ops[l].dst = (int)(r & 7);
-    ops[l].a = (int)((r >> 3) & 7);
-    ops[l].b = (int)((r >> 6) & 7);
-    ops[l].imm = ops[l].kind == OP_CONST ? (splitmix64(&st) >> 1) : 0;
-    ops[l].nabs = 0;
-    if (ops[l].kind == OP_ABSORB) {
-      ops[l].nabs = 1 + (int)((r >> 9) % 3);
-      for (int i = 0; i < 3; i++) ops[l].abs_regs[i] = (int)((r >> (12 + 3 * i)) & 7);
+    synth_op *o = &ops[l];
+    memset(o, 0, sizeof *o);
+    o->kind = cycle[l % (size_t)clen];
+    o->dst = (int)(r & 7);
+    if (flags & SYN_RAM) o->dst %= RAM_ADDR_REG;
+    o->a = (int)((r >> 3) & 7);
+    o->b = (int)((r >> 6) & 7);
+    o->imm = o->kind == OP_CONST ? (splitmix64(&st) >> 1) : 0;
+    if (o->kind == OP_ABSORB) {
+      o->nabs = 1 + (int)((r >> 9) % 3);
+      for (int i = 0; i < 3; i++) o->abs_regs[i] = (int)((r >> (12 + 3 * i)) & 7);
+    } else if (o->kind == OP_CADDR) {
+      o->dst = RAM_ADDR_REG;
+      o->imm = (r >> 9) & 7;
+    } else if (o->kind == OP_LOAD || o->kind == OP_STORE) {
+      o->a = RAM_ADDR_REG;
+      if (o->kind == OP_STORE) o->b = last_dst; /* store the latest result */
+    } else if ((flags & SYN_RAM) && (o->kind == OP_ADD || o->kind == OP_MUL)) {
+      o->a = last_dst;
     }
+    if (o->kind != OP_STORE && o->kind != OP_ABSORB && o->kind != OP_CADDR) last_dst = o->dst;
   }
+  if ((flags & SYN_MERKLE) && levels >= 8) {
+    uint64_t r = splitmix64(&st);
+    synth_op m[5] = {{OP_CONST, 5, 0, 0, r & 1, 0, {0}}, {OP_CONST, 6, 0, 0, (r >> 1) & 1, 0, {0}},
+                     {OP_MFIRST, 0, 5, 1, 0, 0, {0}}, {OP_MSTEP, 0, 6, 2, 0, 0, {0}}, {OP_MLAST, 0, 5, 3, 0, 0, {0}}};
+    for (int i = 0; i < 5; i++) ops[1 + i] = m[i]; /* MerkleStep*: dst = leaf reg, a = dir reg, b = sib reg */
+  }
+  memset(&ops[levels - 1], 0, sizeof ops[levels - 1]);
   ops[levels - 1].kind = OP_END;
-  ops[levels - 1].dst = ops[levels - 1].a = ops[levels - 1].b = 0;
-  ops[levels - 1].imm = 0;
 }
 
 static void set_fe(zkl_f128 *t, size_t n, int col, size_t row, fe v) {
@@ -118,24 +155,102 @@ static void set_sponge_sel(zkl_f128 *t, size_t n, const zk_cols *c, size_t row, 
   }
 }
 
+/* RamTraceBuilder::fill_table (vm/trace/ram.rs:43-271) */
+static int cmp_event(const void *x, const void *y) {
+  const fe *a = (const fe *)x, *b = (const fe *)y;
+  if (a[0] != b[0]) return a[0] < b[0] ? -1 : 1;
+  return (a[1] > b[1]) - (a[1] < b[1]);
+}
+static void ram_fill(zkl_f128 *t, size_t n, const zk_cols *c, const uint8_t pid[32], fe (*ev)[4], size_t n_ev) {
+  qsort(ev, n_ev, sizeof *ev, cmp_event); /* (addr, clk) keys are unique: one event per level */
+  size_t *ev_row = (size_t *)malloc((n_ev + 1) * sizeof(size_t));
+  size_t k = 0;
+  for (size_t row = 0; row < n; row++) {
+    size_t pos = row % 32;
+    if (pos >= 29 && k < n_ev) { /* pad rows hold the sorted table */
+      set_fe(t, n, c->ram_sorted, row, 1);
+      set_fe(t, n, c->ram_s_addr, row, ev[k][0]);
+      set_fe(t, n, c->ram_s_clk, row, ev[k][1]);
+      set_fe(t, n, c->ram_s_val, row, ev[k][2]);
+      set_fe(t, n, c->ram_s_is_write, row, ev[k][3]);
+      ev_row[k++] = row;
+    }
+  }
+  for (size_t i = 0; i + 1 < n_ev; i++) { /* mirror same-address witnesses across the gap */
+    if (ev[i][0] != ev[i + 1][0]) continue;
+    for (size_t row = ev_row[i] + 1; row < ev_row[i + 1]; row++)
+      if (!get_fe(t, n, c->ram_sorted, row)) {
+        set_fe(t, n, c->ram_s_addr, row, ev[i][0]);
+        set_fe(t, n, c->ram_s_clk, row, ev[i][1]);
+        set_fe(t, n, c->ram_s_val, row, ev[i][2]);
+        set_fe(t, n, c->ram_s_is_write, row, ev[i][3]);
+      }
+  }
+  free(ev_row);
+  fe fc[2];
+  program_field_commitment(pid, fc);
+  fe q0 = fc[0], q2 = fe_mul(q0, q0), q3 = fe_mul(q2, q0), q4 = fe_mul(q2, q2), q5 = fe_mul(q4, q0);
+  fe r1 = fe_add(q2, 1), r2 = fe_add(q3, q0), r3 = fe_add(q5, 7);
+  fe gp = 0, last = 0;
+  for (size_t row = 0; row < n; row++) {
+    if (row > 0 && get_fe(t, n, c->ram_sorted, row - 1)) {
+      size_t p = row - 1;
+      fe a = get_fe(t, n, c->ram_s_addr, p), clk = get_fe(t, n, c->ram_s_clk, p), v = get_fe(t, n, c->ram_s_val, p),
+         w = get_fe(t, n, c->ram_s_is_write, p);
+      gp = fe_add(gp, fe_add(fe_add(fe_add(a, fe_mul(r1, clk)), fe_mul(r2, v)), fe_mul(r3, w)));
+      if (get_fe(t, n, c->ram_s_addr, row) == a) last = fe_add(fe_mul(fe_sub(1, w), last), fe_mul(w, v));
+      else last = fe_mul(w, v);
+    }
+    set_fe(t, n, c->ram_gp_sorted, row, gp);
+    set_fe(t, n, c->ram_s_last_write, row, last);
+  }
+  for (size_t row = 0; row + 1 < n; row++) {
+    if (!get_fe(t, n, c->ram_sorted, row)) continue;
+    fe a = get_fe(t, n, c->ram_s_addr, row), an = get_fe(t, n, c->ram_s_addr, row + 1);
+    set_fe(t, n, c->eq_inv, row, fe_inv(fe_sub(an, a)));
+    if (get_fe(t, n, c->ram_sorted, row + 1) && an == a) {
+      fe clk = get_fe(t, n, c->ram_s_clk, row), clk_n = get_fe(t, n, c->ram_s_clk, row + 1);
+      fe delta = clk_n > clk ? clk_n - clk : 0; /* as_int saturating_sub */
+      for (int i = 0; i < 32; i++) set_fe(t, n, c->gadget_b + i, row, (delta >> i) & 1);
+    }
+  }
+  fe gu = 0;
+  for (size_t row = 0; row < n; row++) {
+    if (row > 0 && (row - 1) % 32 == 28) {
+      size_t p = row - 1;
+      int ld = get_fe(t, n, c->op[15], p) == 1, stv = get_fe(t, n, c->op[16], p) == 1;
+      if (ld || stv) {
+        fe a_ev = 0, b_ev = 0;
+        for (int i = 0; i < NR; i++) {
+          fe ri = get_fe(t, n, c->r_start + i, p);
+          a_ev = fe_add(a_ev, fe_mul(get_fe(t, n, c->sel_a + i, p), ri));
+          b_ev = fe_add(b_ev, fe_mul(get_fe(t, n, c->sel_b + i, p), ri));
+        }
+        fe w = stv ? 1 : 0;
+        fe val = stv ? b_ev : get_fe(t, n, c->imm, p);
+        gu = fe_add(gu, fe_add(fe_add(fe_add(a_ev, fe_mul(r1, get_fe(t, n, c->pc, p))), fe_mul(r2, val)), fe_mul(r3, w)));
+      }
+    }
+    set_fe(t, n, c->ram_gp_unsorted, row, gu);
+  }
+}
+
 int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f128 *t, zkl_air_public_inputs *pi,
                             uint32_t *width_out) {
-  if (log_n < 5 || log_n > 26) return -1;
+  if (log_n < 5 || log_n > 26 || (flags & ~7u)) return -1;
+  if ((flags & SYN_MERKLE) && log_n < 8) return -1;
   size_t n = (size_t)1 << log_n, levels = n / 32;
   zk_cols c;
-  cols_for_config(1, 0, 0, 0, 1, &c);
+  cols_for_config(1, !!(flags & SYN_RAM), 0, !!(flags & SYN_MERKLE), 1, &c);
   if (width_out) *width_out = (uint32_t)c.width;
   if (!t) return 0;
   memset(t, 0, (size_t)c.width * n * sizeof(zkl_f128));
   memset(pi, 0, sizeof *pi);
 
-  char desc[128];
-  if (flags & 1)
-    snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 sponge seed=0x%016llx levels=%zu",
-             (unsigned long long)seed, levels);
-  else
-    snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 seed=0x%016llx levels=%zu",
-             (unsigned long long)seed, levels);
+  char desc[160];
+  snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 %s%s%sseed=0x%016llx levels=%zu",
+           (flags & SYN_SPONGE) ? "sponge " : "", (flags & SYN_RAM) ? "ram " : "", (flags & SYN_MERKLE) ? "merkle " : "",
+           (unsigned long long)seed, levels);
   uint8_t pid[32];
   orc_blake3((const uint8_t *)desc, strlen(desc), pid);
   pos_suite ps;
@@ -157,6 +272,11 @@ int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f
   /* VmTraceBuilder (vm.rs:58-888) */
   fe regs[NR] = {0};
   int pending[10], npending = 0;
+  /* RAM: host memory (addr -> value) and the event log (addr, clk, val, is_write) */
+  size_t n_ev = 0, n_mem = 0;
+  fe (*ev)[4] = (fe(*)[4])malloc((levels + 1) * sizeof *ev);
+  fe (*mem)[2] = (fe(*)[2])malloc((levels + 1) * sizeof *mem);
+  int last_merkle = -1;
   for (size_t l = 0; l < levels; l++) {
     fe next[NR];
     memcpy(next, regs, sizeof next);
@@ -173,6 +293,9 @@ int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f
       case OP_NEG: onehot = 5; break;
       case OP_ABSORB:
       case OP_SQUEEZE: onehot = 8; break;
+      case OP_CADDR: onehot = 0; break;
+      case OP_LOAD: onehot = 15; break;
+      case OP_STORE: onehot = 16; break;
       default: break;
     }
     if (onehot >= 0) set_fe(t, n, c.rom_op_start + onehot, rm, 1);
@@ -200,16 +323,64 @@ int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f
         for (size_t r = b; r < b + 32; r++) set_fe(t, n, c.pose_active, r, 1);
       }
     }
-    for (int q = 0; q < 2 && onehot >= 0 && onehot != 8; q++) {
+    if (op->kind == OP_MFIRST || op->kind == OP_MSTEP || op->kind == OP_MLAST) {
+      /* MerkleStepFirst / MerkleStep / MerkleStepLast (vm.rs:675-800) */
+      for (size_t r = b; r < b + 32; r++) set_fe(t, n, c.merkle_g, r, 1);
+      fe acc;
+      if (op->kind == OP_MFIRST) {
+        acc = regs[op->dst];
+        set_fe(t, n, c.merkle_first, rm, 1);
+        set_fe(t, n, c.merkle_leaf, rm, acc);
+      } else {
+        acc = last_merkle >= 0 ? get_fe(t, n, c.merkle_acc, (size_t)last_merkle * 32 + 28) : 0;
+      }
+      for (size_t r = rm; r < rf; r++) set_fe(t, n, c.merkle_acc, r, acc);
+      fe d = regs[op->a], sib = regs[op->b];
+      set_fe(t, n, c.merkle_dir, rm, d);
+      set_fe(t, n, c.merkle_sib, rm, sib);
+      fe in[2] = {fe_add(fe_mul(fe_sub(1, d), acc), fe_mul(d, sib)), fe_add(fe_mul(fe_sub(1, d), sib), fe_mul(d, acc))};
+      apply_level_absorb(t, n, &c, &ps, l, in, 2);
+      if (op->kind == OP_MLAST) set_fe(t, n, c.merkle_last, rf, 1);
+      fe out = get_fe(t, n, c.lanes_start, rf);
+      for (size_t r = rf; r < b + 32; r++) set_fe(t, n, c.merkle_acc, r, out);
+      for (size_t r = b; r < b + 32; r++) set_fe(t, n, c.pose_active, r, 1);
+      last_merkle = (int)l;
+    }
+    if (op->kind == OP_LOAD || op->kind == OP_STORE) {
+      /* Load / Store (vm.rs:803-842): clk = level, loads read 0 from unwritten addresses */
+      fe addr = regs[op->a], val = 0;
+      size_t k = 0;
+      while (k < n_mem && mem[k][0] != addr) k++;
+      for (int q = 0; q < 2; q++) {
+        set_fe(t, n, c.op[onehot], rows[q], 1);
+        set_sel(t, n, rows[q], c.sel_a, op->a);
+        if (op->kind == OP_LOAD) set_sel(t, n, rows[q], c.sel_dst0, op->dst);
+        else set_sel(t, n, rows[q], c.sel_b, op->b);
+      }
+      if (op->kind == OP_LOAD) {
+        val = k < n_mem ? mem[k][1] : 0;
+        set_fe(t, n, c.imm, rm, val);
+        set_fe(t, n, c.imm, rf, val);
+        next[op->dst] = val;
+      } else {
+        val = regs[op->b];
+        if (k == n_mem) { mem[k][0] = addr; n_mem++; }
+        mem[k][1] = val;
+      }
+      ev[n_ev][0] = addr; ev[n_ev][1] = (fe)l; ev[n_ev][2] = val; ev[n_ev][3] = op->kind == OP_STORE;
+      n_ev++;
+    }
+    for (int q = 0; q < 2 && onehot >= 0 && onehot != 8 && onehot < 15; q++) {
       size_t row = rows[q];
       set_fe(t, n, c.op[onehot], row, 1);
       set_sel(t, n, row, c.sel_dst0, op->dst);
-      if (op->kind == OP_CONST) set_fe(t, n, c.imm, row, (fe)op->imm);
-      if (op->kind != OP_CONST) set_sel(t, n, row, c.sel_a, op->a);
+      if (op->kind == OP_CONST || op->kind == OP_CADDR) set_fe(t, n, c.imm, row, (fe)op->imm);
+      else set_sel(t, n, row, c.sel_a, op->a);
       if (op->kind == OP_ADD || op->kind == OP_SUB || op->kind == OP_MUL) set_sel(t, n, row, c.sel_b, op->b);
     }
     switch (op->kind) {
-      case OP_CONST: next[op->dst] = (fe)op->imm; break;
+      case OP_CONST:
+      case OP_CADDR: next[op->dst] = (fe)op->imm; break;
       case OP_MOV: next[op->dst] = regs[op->a]; break;
       case OP_ADD: next[op->dst] = fe_add(regs[op->a], regs[op->b]); break;
       case OP_SUB: next[op->dst] = fe_sub(regs[op->a], regs[op->b]); break;
@@ -223,6 +394,9 @@ int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f
       for (int i = 0; i < NR; i++) set_fe(t, n, c.r_start + i, r, next[i]);
     memcpy(regs, next, sizeof regs);
   }
+  if (flags & SYN_RAM) ram_fill(t, n, &c, pid, ev, n_ev);
+  free(ev);
+  free(mem);
   /* RomTraceBuilder (rom.rs:37-106) */
   fe rc3[POS_ROUNDS][3], mds3[3][3], w0[59], w1[59];
   rom_constants(pid, rc3, mds3);
@@ -262,7 +436,12 @@ int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f
   /* AIR public inputs (prove.rs:292-423 with segment = whole trace) */
   memcpy(pi->program_id, pid, 32);
   memcpy(pi->program_commitment, pid, 32);
-  pi->feature_mask = (flags & 1) ? 2 | 32 | 1 : 2; /* FM_VM (+ FM_SPONGE | FM_POSEIDON) */
+  pi->feature_mask = FM_VM | ((flags & SYN_SPONGE) ? FM_SPONGE | FM_POSEIDON : 0) | ((flags & SYN_RAM) ? FM_RAM : 0) |
+                     ((flags & SYN_MERKLE) ? FM_MERKLE | FM_POSEIDON : 0);
+  if (flags & SYN_MERKLE) { /* root = acc after the MerkleStepLast level, as 16 LE bytes (utils.rs:346-355) */
+    fe root = get_fe(t, n, c.merkle_acc, 5 * 32 + 28);
+    for (int i = 0; i < 16; i++) pi->merkle_root[i] = (uint8_t)(root >> (8 * i));
+  }
   pi->segment_feature_mask = pi->feature_mask;
   pi->n_main_slots = 0;
   /* vm_output_from_trace_with_layout (utils.rs:262-289) */
@@ -296,7 +475,15 @@ int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f
     if (at_final && get_fe(t, n, c.op[6], r)) mask |= 1u << 6;
     if (get_fe(t, n, c.op[8], r)) mask |= 1u << 7;
   }
+  uint32_t ram_bits = 0;
+  if (flags & SYN_RAM)
+    for (size_t r = 0; r + 1 < n; r++)
+      if (get_fe(t, n, c.ram_sorted, r) && get_fe(t, n, c.ram_sorted, r + 1) &&
+          get_fe(t, n, c.ram_s_addr, r) == get_fe(t, n, c.ram_s_addr, r + 1)) {
+        mask |= 1u << 8;
+        for (int i = 0; i < 32; i++) if (get_fe(t, n, c.gadget_b + i, r)) ram_bits |= 1u << i;
+      }
   pi->vm_usage_mask = mask;
-  pi->ram_delta_clk_bits = 0;
+  pi->ram_delta_clk_bits = ram_bits;
   return 0;
 }

@@ -37,13 +37,21 @@ def test_select_partitions():
         assert zkl_hip.select_partitions_for_trace(w, n) == exp
 
 
-@pytest.mark.parametrize("flags", [0, 1])
+WIDTHS = {0: 204, 1: 204, 2: 212, 3: 212, 4: 211, 5: 211, 6: 219, 7: 219}
+
+
+@pytest.mark.parametrize("flags", range(8))
 @pytest.mark.parametrize("log_n", [5, 6, 8, 10, 12])
 def test_product_tracegen_matches_oracle(oracle, log_n, flags):
+    """Generator flags: 1 sponge, 2 RAM, 4 Merkle (needs log_n >= 8)."""
     import zkl_hip
+    if flags & 4 and log_n < 8:
+        with pytest.raises(zkl_hip.ZklError):
+            zkl_hip.synth_vm_segment(0x5EED0001 + log_n, log_n, flags)
+        return
     t1, pi1, w1 = zkl_hip.synth_vm_segment(0x5EED0001 + log_n, log_n, flags)
     t2, pi2, w2 = oracle.synth_segment(0x5EED0001 + log_n, log_n, flags)
-    assert w1 == w2 == 204
+    assert w1 == w2 == WIDTHS[flags]
     assert bytes(t1) == bytes(t2)
     assert bytes(pi1) == bytes(pi2)
 

@@ -89,6 +89,64 @@ def test_sponge_full_size_verifies(oracle, gpu_ctx):
     assert rc == 0, err
 
 
+@pytest.mark.parametrize("flags,log_n,q,blowup,grind", [
+    (2, 8, 32, 16, 4),     # RAM: {vm, ram, rom}, W = 212
+    (2, 11, 64, 16, 10),   # RAM with the delta_clk gadget over several bits
+    (4, 8, 16, 8, 2),      # Merkle path: {vm, merkle, rom}, W = 211
+    (6, 10, 64, 16, 8),    # RAM + Merkle: baseline layout W = 219
+    (7, 9, 48, 32, 6),     # sponge + RAM + Merkle
+    (3, 12, 64, 16, 12),   # sponge + RAM
+])
+def test_ram_merkle_proof_bytes_match_oracle(oracle, gpu_ctx, flags, log_n, q, blowup, grind):
+    """RamAir (ram.rs:82-236) and MerkleAir (merkle.rs:60-134) blocks on the GPU evaluator."""
+    import zkl_hip
+    oracle.set_threads(16 if log_n >= 10 else 1)
+    n = 1 << log_n
+    seed = 0x5EED0500 + 16 * flags + log_n
+    t, pi, w = zkl_hip.synth_vm_segment(seed, log_n, flags)
+    opts = zkl_hip.proof_options(w, n, queries=q, blowup=blowup, grind=grind)
+    got = gpu_ctx.prove_segment(t, w, n, pi, opts)
+    ot, opi, _ = oracle.synth_segment(seed, log_n, flags)
+    oo = oracle.ProofOptions(*[getattr(opts, f) for f, _ in opts._fields_])
+    want = oracle.prove(ot, w, n, opi, oo)
+    oracle.set_threads(1)
+    assert got == want
+    rc, err = oracle.verify(got, opi, oo)
+    assert rc == 0, err
+
+
+def test_ram_merkle_bad_witness_rejected(gpu_ctx):
+    """A wrong Merkle root in the public inputs and a corrupted RAM read are both caught."""
+    import zkl_hip
+    n = 1 << 8
+    t, pi, w = zkl_hip.synth_vm_segment(0x5EED0601, 8, 6)
+    opts = zkl_hip.proof_options(w, n, queries=8, grind=0)
+    pi.merkle_root[3] ^= 0x10
+    with pytest.raises(zkl_hip.ZklError, match="degree too large"):
+        gpu_ctx.prove_segment(t, w, n, pi, opts)
+    pi.merkle_root[3] ^= 0x10
+    s_on, s_val, s_w = 149, 152, 153
+    row = next(r for r in range(n) if t[s_on * n + r].lo == 1 and t[s_w * n + r].lo == 0
+               and (t[s_val * n + r].lo | t[s_val * n + r].hi))
+    t[s_val * n + row].lo ^= 1
+    with pytest.raises(zkl_hip.ZklError, match="degree too large"):
+        gpu_ctx.prove_segment(t, w, n, pi, opts)
+
+
+def test_ram_full_size_verifies(oracle, gpu_ctx):
+    """configs[1] shape (2^16 rows, blowup 16, q 64, grind 16) with sponge + RAM + Merkle."""
+    import zkl_hip
+    n = 1 << 16
+    t, pi, w = zkl_hip.synth_vm_segment(0x5EED0700, 16, 7)
+    assert w == 219
+    opts = zkl_hip.proof_options(w, n)
+    got = gpu_ctx.prove_segment(t, w, n, pi, opts)
+    oo = oracle.ProofOptions(*[getattr(opts, f) for f, _ in opts._fields_])
+    _, opi, _ = oracle.synth_segment(0x5EED0700, 16, 7)
+    rc, err = oracle.verify(got, opi, oo)
+    assert rc == 0, err
+
+
 def test_multi_partition_parity(oracle, gpu_ctx):
     """n = 2^14 exercises 2-way row partitioning + merge_many (PartitionOptions)."""
     import zkl_hip

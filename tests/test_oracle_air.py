@@ -58,3 +58,61 @@ def test_sponge_trace_proves_and_verifies(oracle):
     proof = oracle.prove(t, w, n, pi, opts)
     rc, err = oracle.verify(proof, pi, opts)
     assert rc == 0, err
+
+
+# generator flags: 1 sponge, 2 RAM (Load/Store), 4 Merkle path
+@pytest.mark.parametrize("flags,width", [(2, 212), (4, 211), (3, 212), (5, 211), (6, 219), (7, 219)])
+@pytest.mark.parametrize("log_n", [8, 11])
+def test_ram_merkle_traces_satisfy_air(oracle, flags, width, log_n):
+    """RamAir (ram.rs:82-236) and MerkleAir (merkle.rs:60-134) blocks, with the segment
+    layouts {vm, ram, rom} = 212, {vm, merkle, rom} = 211 and the baseline 219."""
+    n = 1 << log_n
+    t, pi, w = oracle.synth_segment(0x5EED0300 + flags, log_n, flags)
+    assert w == width
+    rc, n_tc, n_as, ceb, ncomp = oracle.air_info(pi, w, n)
+    assert rc == 0 and (ceb, ncomp) == (8, 7)
+    n_ram = 0
+    if flags & 2:
+        n_ram = 7 + ((bin(pi.ram_delta_clk_bits).count("1") + 1) if pi.vm_usage_mask & 0x100 else 0)
+    n_pose = 27 * 12 + 12 + (10 if flags & 1 else 0) if flags & 5 else 0
+    n_sponge_sel = 40 if flags & 1 else 0
+    assert n_tc == 193 + n_ram + (7 if flags & 4 else 0) + n_pose + n_sponge_sel
+    assert oracle.check_trace(t, pi, w, n) == (0, 0, 0)
+
+
+def test_ram_trace_uses_delta_clk_gadget(oracle):
+    n = 1 << 12
+    t, pi, w = oracle.synth_segment(0x5EED0001, 12, 2)
+    assert pi.vm_usage_mask & 0x100 and bin(pi.ram_delta_clk_bits).count("1") >= 3
+    assert oracle.check_trace(t, pi, w, n) == (0, 0, 0)
+
+
+def test_ram_corruption_detected(oracle):
+    """A read whose sorted-table value differs from the last write to that address."""
+    n = 1 << 9
+    t, pi, w = oracle.synth_segment(0x5EED0301, 9, 2)
+    s_on, s_val, s_w = 149, 152, 153          # {vm, ram, rom} layout (layout.rs:247-256)
+    row = next(r for r in range(n) if t[s_on * n + r].lo == 1 and t[s_w * n + r].lo == 0
+               and (t[s_val * n + r].lo | t[s_val * n + r].hi))
+    t[s_val * n + row].lo ^= 1
+    rc, bad_row, idx = oracle.check_trace(t, pi, w, n)
+    assert rc == 1
+
+
+def test_merkle_root_binding(oracle):
+    n = 256
+    t, pi, w = oracle.synth_segment(0x99, 8, 4)
+    assert pi.feature_mask == 0x43
+    pi.merkle_root[0] ^= 1
+    rc, bad_row, idx = oracle.check_trace(t, pi, w, n)
+    assert rc == 1 and bad_row == 5 * 32 + 28      # MerkleStepLast final row
+
+
+@pytest.mark.parametrize("flags", [2, 4, 7])
+def test_ram_merkle_proves_and_verifies(oracle, flags):
+    n = 1 << 8
+    t, pi, w = oracle.synth_segment(0x5EED0400 + flags, 8, flags)
+    opts = oracle.default_options(w, n, queries=16, grind=4)
+    proof = oracle.prove(t, w, n, pi, opts)
+    rc, err = oracle.verify(proof, pi, opts)
+    assert rc == 0, err

@@ -13,8 +13,7 @@ namespace zkl {
 static constexpr int NR = 8;
 static constexpr int ROUNDS = 27;
 static constexpr int STEPS = 32;
-static constexpr uint64_t FM_POSEIDON = 1, FM_VM = 2, FM_VM_EXPECT = 16, FM_SPONGE = 32, FM_MERKLE = 64, FM_RAM = 128;
-enum { U_ASSERT = 0, U_ASSERT_BIT, U_ASSERT_RANGE, U_DIVMOD, U_MULWIDE, U_DIV128, U_EQ, U_SPONGE };
+enum { U_ASSERT = 0, U_ASSERT_BIT, U_ASSERT_RANGE, U_DIVMOD, U_MULWIDE, U_DIV128, U_EQ, U_SPONGE, U_RAM_DCLK };
 
 fe fe_from(const zkl_f128& v) { return fe{v.lo, v.hi}; }
 zkl_f128 to_abi(fe v) { return zkl_f128{v.lo, v.hi}; }
@@ -48,7 +47,11 @@ Layout make_layout(bool vm, bool ram, bool sponge, bool merkle, bool rom) {
   cur += 40;
   c.imm = cur; c.eq_inv = cur + 1;
   cur += 2;
+  c.ram_sorted = cur; c.ram_s_addr = cur + 1; c.ram_s_clk = cur + 2; c.ram_s_val = cur + 3;
+  c.ram_s_is_write = cur + 4; c.ram_s_last_write = cur + 5; c.ram_gp_unsorted = cur + 6; c.ram_gp_sorted = cur + 7;
   if (ram) cur += 8;
+  c.merkle_g = cur; c.merkle_dir = cur + 1; c.merkle_sib = cur + 2; c.merkle_acc = cur + 3;
+  c.merkle_first = cur + 4; c.merkle_last = cur + 5; c.merkle_leaf = cur + 6;
   if (merkle) cur += 7;
   c.pi_prog = cur++;
   c.pc = cur++;
@@ -74,8 +77,6 @@ std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n,
   uint64_t eff = pi.segment_feature_mask ? pi.segment_feature_mask : pi.feature_mask;
   bool f_pose = eff & FM_POSEIDON, f_vm = eff & FM_VM, f_exp = eff & FM_VM_EXPECT, f_sponge = eff & FM_SPONGE,
        f_merkle = eff & FM_MERKLE, f_ram = eff & FM_RAM;
-  if (f_merkle || f_ram)
-    return "segment feature mask enables RAM/Merkle AIR blocks, which this backend does not implement yet";
   bool pid_nz = false, com_nz = false;
   for (int i = 0; i < 32; i++) { pid_nz |= pi.program_id[i] != 0; com_nz |= pi.program_commitment[i] != 0; }
   Layout base = make_layout(true, true, true, true, true);
@@ -103,10 +104,26 @@ std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n,
     for (int k = 0; k < 12; k++) d.pose_mds[i][k] = ps.mds[i][k];
   for (int r = 0; r < 27; r++)
     for (int i = 0; i < 12; i++) d.pose_rc[r][i] = ps.rc[r][i];
+  d.ram_block = f_ram;
+  d.ram_dclk = f_ram && (m & (1u << U_RAM_DCLK));
+  d.ram_dclk_bits = pi.ram_delta_clk_bits;
+  {
+    fe pfe[2] = {fe_zero(), fe_zero()};
+    if (pid_nz) program_field_commitment(pi.program_id, pfe);  // vm/air/mod.rs:184-188
+    fe q0 = pfe[0], q2 = fe_mul(q0, q0), q3 = fe_mul(q2, q0), q5 = fe_mul(fe_mul(q2, q2), q0);
+    d.ram_r[0] = fe_add(q2, fe_one());
+    d.ram_r[1] = fe_add(q3, q0);
+    d.ram_r[2] = fe_add(q5, fe{7, 0});
+  }
+  d.merkle_block = f_merkle;
+  d.merkle_root = be_from_le16(pi.merkle_root);
 
-  // degrees in module order: Poseidon, Ctrl, ALU (vm), ROM (vm/air/mod.rs:217-238)
+  // degrees in module order: Poseidon, Ctrl, ALU (vm), RAM, Merkle, ROM (vm/air/mod.rs:217-238)
   auto& deg = A.degree_base;
-  auto push = [&](int cnt, int b) { for (int i = 0; i < cnt; i++) deg.push_back(b); };
+  auto& cyc = A.degree_cycle;
+  auto push = [&](int cnt, int b, int c = 1) {
+    for (int i = 0; i < cnt; i++) { deg.push_back(b); cyc.push_back(c); }
+  };
   if (f_pose) {  // PoseidonAir::push_degrees (poseidon.rs:26-62)
     push(27 * 12, 4);
     push(12, 1);
@@ -125,14 +142,26 @@ std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n,
     if (m & (1u << U_MULWIDE)) push(1, 5);
     if (m & (1u << U_DIV128)) push(2, 5);
   }
+  if (f_ram) {  // RamAir::push_degrees (ram.rs:26-79): only the unsorted carry has the cycle
+    push(1, 4); push(1, 2, 0); push(1, 5, 0); push(1, 3, 0); push(1, 6, 0); push(1, 5, 0);
+    if (d.ram_dclk) { push(__builtin_popcount(pi.ram_delta_clk_bits), 5, 0); push(1, 5, 0); }
+    push(1, 2, 0);
+  }
+  if (f_merkle) { push(3, 3); push(1, 2); push(3, 3); }  // MerkleAir (merkle.rs:26-58)
   if (pid_nz) { push(81, 3); push(3, 1); push(2, 1); }
   if (deg.empty()) return "AIR without transition constraints is not a VM segment";
   A.n_tc = d.n_tc = (int)deg.size();
-  int maxb = *std::max_element(deg.begin(), deg.end());
-  int ceb = 1;
-  while (ceb < maxb) ceb <<= 1;  // (base + #cycles - 1).next_power_of_two(), min 2
-  A.ce_blowup = std::max(ceb, 2);
-  size_t max_eval = (size_t)maxb * (n - 1) + (n / STEPS) * (STEPS - 1);
+  // ce_blowup = max (base + #cycles - 1).next_power_of_two(), min 2; eval degree
+  // base (n-1) + #cycles (n/32) 31 (winter-air TransitionConstraintDegree)
+  int ceb = 2;
+  size_t max_eval = 0;
+  for (size_t i = 0; i < deg.size(); i++) {
+    int need = 1;
+    while (need < deg[i] + cyc[i] - 1) need <<= 1;
+    ceb = std::max(ceb, need);
+    max_eval = std::max(max_eval, (size_t)deg[i] * (n - 1) + (cyc[i] ? (n / STEPS) * (STEPS - 1) : 0));
+  }
+  A.ce_blowup = ceb;
   A.num_comp_cols = (int)((max_eval - (n - 1) + n - 1) / n);
 
   // ---- assertions (ScheduleAir, VM PI, RomAir), dedup by (col, step), Winterfell order

@@ -10,12 +10,18 @@
 
 namespace zkl {
 
+// feature bits (zk-lisp-proof/src/pi.rs:23-28)
+constexpr uint64_t FM_POSEIDON = 1, FM_VM = 2, FM_VM_EXPECT = 16, FM_SPONGE = 32, FM_MERKLE = 64, FM_RAM = 128;
+
 // Columns::for_config (vm/layout.rs:183-374)
 struct Layout {
   int lanes_start, g_map, g_final, g_r_start, mask, r_start;
   int op[17];  // const mov add sub mul neg eq select sponge assert assert_bit assert_range divmod div128 mulwide load store
   int sel_dst0, sel_a, sel_b, sel_c, sel_dst1, sel_s_bits, sel_s_active, imm, eq_inv;
   int pi_prog, pc, rom_op_start, pose_active, gadget_b, rom_s;
+  int ram_sorted, ram_s_addr, ram_s_clk, ram_s_val, ram_s_is_write, ram_s_last_write, ram_gp_unsorted,
+      ram_gp_sorted;                                                             // layout.rs:247-256
+  int merkle_g, merkle_dir, merkle_sib, merkle_acc, merkle_first, merkle_last, merkle_leaf;  // :262-270
   int width;
 };
 Layout make_layout(bool vm, bool ram, bool sponge, bool merkle, bool rom);
@@ -26,6 +32,10 @@ struct AirDevice {
   int feat_vm, sponge_block, commit_nonzero, n_tc;
   int pose_block, pose_bind;  // PoseidonAir present; its VM->lane bindings present
   uint32_t vm_usage_mask;
+  int ram_block, ram_dclk, merkle_block;  // RamAir / its delta_clk gadget / MerkleAir present
+  uint32_t ram_dclk_bits;                 // pi.ram_delta_clk_bits (bits with a booleanity constraint)
+  fe ram_r[3];                            // compressor coefficients r1, r2, r3 (ram.rs:112-121)
+  fe merkle_root;                         // be_from_le8(pi.merkle_root) (merkle.rs:118)
   fe pose_mds[12][12];  // AIR Poseidon suite (suite_id = program_id, vm/air/mod.rs:129-137)
   fe pose_rc[27][12];
   fe rom_mds[3][3];
@@ -43,7 +53,8 @@ struct AirInstance {
   AirDevice dev;
   size_t n = 0;
   int ce_blowup = 0, num_comp_cols = 0, n_tc = 0;
-  std::vector<int> degree_base;          // per transition constraint (all with one 32-cycle)
+  std::vector<int> degree_base;          // per transition constraint
+  std::vector<int> degree_cycle;         // 1 if the constraint carries the 32-row cycle
   std::vector<Assertion> assertions;     // deduped, Winterfell order (step, column)
   fe suite_dom[2];
 };

@@ -790,9 +790,9 @@ struct Acc {
   __device__ __forceinline__ void emit(fe v) { mul_acc(al[ix++], v, a); }
 };
 
-// POSE: the PoseidonAir block is compiled into a separate instance so that VM-only segments
-// keep the smaller register footprint
-template <bool POSE>
+// POSE: the PoseidonAir block, RM: the RamAir / MerkleAir blocks; each is compiled into a
+// separate instance so that VM-only segments keep the smaller register footprint
+template <bool POSE, bool RM>
 __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restrict__ lde, const fe* __restrict__ roots,
                                                               int roots_shift, const fe* __restrict__ pertab,
                                                               const fe* __restrict__ bm,
@@ -1011,6 +1011,67 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
       A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[ARANGE], eqt)), s_eq));
     }
   }
+  if (RM && c_air.ram_block) {
+    // ---------------- RamAir (ram.rs:82-236)
+    const fe g_hold = fe_sub_sel(p_pad, p_pad_last);
+    const fe op_load = cur(C.op[15]), op_store = cur(C.op[16]);
+    const fe event = fe_mul(p_final, fe_add_sel(op_load, op_store));
+    const fe r1 = c_air.ram_r[0], r2 = c_air.ram_r[1], r3 = c_air.ram_r[2];
+    fe a_ev = fe_zero(), b_ev = fe_zero();
+    for (int r = 0; r < 8; r++) {
+      const fe rc = cur(C.r_start + r);
+      a_ev = fe_add_sel(a_ev, fe_mul(cur(C.sel_a + r), rc));
+      b_ev = fe_add_sel(b_ev, fe_mul(cur(C.sel_b + r), rc));
+    }
+    const fe val_ev = fe_add_sel(fe_mul(op_store, b_ev), fe_mul(fe_sub_sel(one, op_store), cur(C.imm)));
+    const fe comp_uns =
+        fe_add_sel(fe_add_sel(fe_add_sel(a_ev, fe_mul(r1, cur(C.pc))), fe_mul(r2, val_ev)), fe_mul(r3, op_store));
+    const fe gu = cur(C.ram_gp_unsorted), du = fe_sub_sel(nxt(C.ram_gp_unsorted), gu);
+    A.emit(fe_add_sel(fe_add_sel(fe_mul(event, fe_sub_sel(du, comp_uns)), fe_mul(fe_sub_sel(one, event), du)),
+                      fe_mul(g_hold, du)));
+    const fe s_on = cur(C.ram_sorted), s_addr = cur(C.ram_s_addr), s_clk = cur(C.ram_s_clk), s_val = cur(C.ram_s_val),
+             s_w = cur(C.ram_s_is_write), lastw = cur(C.ram_s_last_write);
+    const fe same = fe_sub_sel(one, fe_mul(fe_sub_sel(nxt(C.ram_s_addr), s_addr), cur(C.eq_inv)));
+    const fe comp = fe_add_sel(fe_add_sel(fe_add_sel(s_addr, fe_mul(r1, s_clk)), fe_mul(r2, s_val)), fe_mul(r3, s_w));
+    const fe gs = cur(C.ram_gp_sorted), ds = fe_sub_sel(nxt(C.ram_gp_sorted), gs);
+    A.emit(fe_add_sel(fe_mul(s_on, fe_sub_sel(ds, comp)), fe_mul(fe_sub_sel(one, s_on), ds)));
+    const fe sw_val = fe_mul(s_w, s_val);
+    const fe keep = fe_add_sel(fe_mul(same, fe_add_sel(fe_mul(fe_sub_sel(one, s_w), lastw), sw_val)),
+                               fe_mul(fe_sub_sel(one, same), sw_val));
+    A.emit(fe_mul(s_on, fe_sub_sel(nxt(C.ram_s_last_write), keep)));
+    A.emit(fe_mul(fe_mul(s_on, fe_sub_sel(one, s_w)), fe_sub_sel(s_val, lastw)));
+    const fe s_on_n = nxt(C.ram_sorted);
+    const fe on2 = fe_mul(s_on, s_on_n);
+    A.emit(fe_mul(fe_mul(fe_mul(on2, fe_sub_sel(one, same)), fe_sub_sel(one, nxt(C.ram_s_is_write))), nxt(C.ram_s_val)));
+    A.emit(fe_mul(s_on, fe_mul(same, fe_sub_sel(same, one))));
+    if (c_air.ram_dclk) {
+      const fe g_same = fe_mul(s_on, same);
+      const uint32_t bits = c_air.ram_dclk_bits;
+      fe sum = fe_zero(), pow2 = one;
+      for (int k = 0; k < 32; k++) {
+        const fe bk = cur(C.gadget_b + k);
+        if ((bits >> k) & 1u) A.emit(fe_mul(g_same, fe_mul(bk, fe_sub_sel(bk, one))));
+        sum = fe_add_sel(sum, fe_mul(pow2, bk));
+        pow2 = fe_add_sel(pow2, pow2);
+      }
+      A.emit(fe_mul(fe_mul(on2, same), fe_sub_sel(fe_sub_sel(nxt(C.ram_s_clk), s_clk), sum)));
+    }
+    A.emit(fe_mul(p_last, fe_sub_sel(gu, gs)));
+  }
+  if (RM && c_air.merkle_block) {
+    // ---------------- MerkleAir (merkle.rs:60-134)
+    const fe g = cur(C.merkle_g), dir = cur(C.merkle_dir), acc = cur(C.merkle_acc), sib = cur(C.merkle_sib);
+    const fe pg = fe_mul(p_map, g);
+    const fe ndir = fe_sub_sel(one, dir);
+    A.emit(fe_mul(pg, fe_mul(dir, fe_sub_sel(dir, one))));
+    A.emit(fe_mul(pg, fe_sub_sel(cur(C.lanes_start), fe_add_sel(fe_mul(ndir, acc), fe_mul(dir, sib)))));
+    A.emit(fe_mul(pg, fe_sub_sel(cur(C.lanes_start + 1), fe_add_sel(fe_mul(ndir, sib), fe_mul(dir, acc)))));
+    const fe acc_n = nxt(C.merkle_acc);
+    A.emit(fe_mul(fe_mul(g, g_carry), fe_sub_sel(acc_n, acc)));
+    A.emit(fe_mul(fe_mul(pg, cur(C.merkle_first)), fe_sub_sel(acc, cur(C.merkle_leaf))));
+    A.emit(fe_mul(fe_mul(fe_mul(p_final, g), cur(C.merkle_last)), fe_sub_sel(acc, c_air.merkle_root)));
+    A.emit(fe_mul(fe_mul(fe_mul(p_pad_last, g), nxt(C.merkle_g)), fe_sub_sel(acc_n, acc)));
+  }
   // ---------------- RomAir (rom.rs:57-120)
   if (c_air.commit_nonzero) {
     fe s3[3];
@@ -1065,15 +1126,19 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
 }
 
 void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab, const fe* d_bm,
-                            const CeParams& p, ProofConsts* dK, bool pose_block, fe* d_out, hipStream_t s) {
+                            const CeParams& p, ProofConsts* dK, bool pose_block, bool ram_merkle, fe* d_out,
+                            hipStream_t s) {
   (void)hipMemcpyAsync(&dK->ce, &p, sizeof p, hipMemcpyHostToDevice, s);
   int shift = ilog2s(Ntab) - ilog2s(p.ce);
-  if (pose_block)
-    constraint_eval_kernel<true><<<(unsigned)((p.ce + 255) / 256), 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm,
-                                                                                 dK, d_out);
+  const unsigned grid = (unsigned)((p.ce + 255) / 256);
+  if (pose_block && ram_merkle)
+    constraint_eval_kernel<true, true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_out);
+  else if (pose_block)
+    constraint_eval_kernel<true, false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_out);
+  else if (ram_merkle)
+    constraint_eval_kernel<false, true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_out);
   else
-    constraint_eval_kernel<false><<<(unsigned)((p.ce + 255) / 256), 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm,
-                                                                                  dK, d_out);
+    constraint_eval_kernel<false, false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_out);
 }
 
 __global__ void boundary_scatter_kernel(const uint32_t* slot, const uint32_t* step, const fe* beta, size_t na, size_t n,

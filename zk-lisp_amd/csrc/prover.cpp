@@ -420,7 +420,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   {
     KScope k(C, KF_CEVAL);
     launch_constraint_eval(C->lde.f(), roots, Ntab, C->pertab.f(), C->bm.f(), cp, dK, air.dev.pose_block != 0,
-                           C->ce.f(), s);
+                           (air.dev.ram_block | air.dev.merkle_block) != 0, C->ce.f(), s);
   }
   T.mark(3);
 
