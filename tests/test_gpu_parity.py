@@ -43,7 +43,7 @@ def test_proof_bytes_match_oracle(oracle, gpu_ctx, log_n, q, blowup, grind):
 
 
 @pytest.mark.parametrize("log_n,q,blowup,grind", [
-    (5, 8, 16, 0), (6, 32, 8, 4), (8, 64, 16, 10), (10, 64, 16, 12), (7, 255, 4, 1),
+    (5, 8, 16, 0), (6, 32, 8, 4), (8, 64, 16, 10), (10, 64, 16, 12), (7, 255, 8, 1),
 ])
 def test_sponge_proof_bytes_match_oracle(oracle, gpu_ctx, log_n, q, blowup, grind):
     """Segments with SAbsorbN / SSqueeze enable the Poseidon AIR block (poseidon.rs:26-162):
