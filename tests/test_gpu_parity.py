@@ -68,8 +68,8 @@ def test_sponge_proof_bytes_match_oracle(oracle, gpu_ctx, log_n, q, blowup, grin
 def test_sponge_bad_lane_rejected(gpu_ctx):
     """A Poseidon lane value off its permutation breaks a round constraint."""
     import zkl_hip
-    n = 1 << 7
-    t, pi, w = zkl_hip.synth_vm_segment(0x5B0A6E07, 7, 1)
+    n = 1 << 8
+    t, pi, w = zkl_hip.synth_vm_segment(0x5B0A6E08, 8, 1)
     t[3 * n + 32 * 3 + 9].lo ^= 1      # lane 3, round row 8 of level 3 (a squeeze level)
     opts = zkl_hip.proof_options(w, n, queries=8, grind=0)
     with pytest.raises(zkl_hip.ZklError, match="degree too large"):
@@ -118,8 +118,8 @@ def test_ram_merkle_proof_bytes_match_oracle(oracle, gpu_ctx, flags, log_n, q, b
 def test_ram_merkle_bad_witness_rejected(gpu_ctx):
     """A wrong Merkle root in the public inputs and a corrupted RAM read are both caught."""
     import zkl_hip
-    n = 1 << 8
-    t, pi, w = zkl_hip.synth_vm_segment(0x5EED0601, 8, 6)
+    n = 1 << 9
+    t, pi, w = zkl_hip.synth_vm_segment(0x5EED0601, 9, 6)
     opts = zkl_hip.proof_options(w, n, queries=8, grind=0)
     pi.merkle_root[3] ^= 0x10
     with pytest.raises(zkl_hip.ZklError, match="degree too large"):
