@@ -11,5 +11,5 @@ timeout -k 10 600 python bench.py --steps 3 --warmup 1 > $out/bench.json 2> $out
 cat $out/bench.json
 export TMPDIR=/tmp
 root=$PWD
-cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $root/$out/prof -o run --output-format csv -- python3 $root/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $root/$out/prof_bench.json 2> $root/$out/prof.err || { echo "rocprof failed rc=$?"; tail -20 $root/$out/prof.err; exit 1; }
+cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $root/$out/prof -o run --output-format csv -- python3 $root/bench.py --steps 2 --warmup 1 --no-cpu-baseline --c3-inflight 1 > $root/$out/prof_bench.json 2> $root/$out/prof.err || { echo "rocprof failed rc=$?"; tail -20 $root/$out/prof.err; exit 1; }
 echo done
