@@ -151,6 +151,14 @@ int zkl_hip_hash_rows(zkl_ctx* ctx, const void* d_matrix, uint32_t n_cols, uint3
 /* MerkleTree::new over n_leaves digests (field-element form); writes all 2*n nodes
  * (nodes[1] = root, nodes[n+i] = leaf i) to d_nodes_out. */
 int zkl_hip_merkle_tree(zkl_ctx* ctx, const void* d_leaves, uint32_t n_leaves, void* d_nodes_out);
+/* n_states Poseidon permutations (poseidon/hasher.rs:173-190, suite [0;32]) of 12-element
+ * canonical states, in place.  engine 1 = matrix-core form (the one the commitment kernels
+ * use on large levels), 0 = lane-group form.  Stage entry point for parity tests. */
+int zkl_hip_poseidon_permute(zkl_ctx* ctx, void* d_states, uint32_t n_states, int engine);
+/* Process-wide hashing policy: engine 1 (default) runs Poseidon levels of at least
+ * pm_min_items states (default 65536) on the matrix-core permutation, engine 0 keeps every
+ * level on lane groups.  Both give identical digests; this only moves time. */
+int zkl_hip_set_hash_policy(int engine, uint32_t pm_min_items);
 /* Coset low-degree extension of column-major n_cols x n_rows evaluations over
  * GENERATOR * <w_{n*blowup}>; writes coefficients (n_cols x n_rows) and the LDE
  * (n_cols x n_rows*blowup), both column-major, natural order. */

@@ -369,3 +369,100 @@ def test_c5_shape_2p20_rows_verifies(oracle, gpu_ctx):
     rc, err = oracle.verify(proof, opi, oo)
     oracle.set_threads(1)
     assert rc == 0, err
+
+
+@pytest.fixture
+def pm_policy(gpu_ctx):
+    """Route every Poseidon level of >= 32 states to the matrix-core permutation, restore the
+    default policy afterwards."""
+    import zkl_hip
+    lib = zkl_hip.load_library()
+    assert lib.zkl_hip_set_hash_policy(1, 32) == 0
+    yield
+    assert lib.zkl_hip_set_hash_policy(1, 1 << 16) == 0
+
+
+def _fe_buf(vals):
+    return (C.c_uint8 * (16 * len(vals))).from_buffer_copy(b"".join(v.to_bytes(16, "little") for v in vals))
+
+
+@pytest.mark.parametrize("engine", [1, 0])
+def test_stage_permute_matches_oracle(oracle, gpu_ctx, engine):
+    """zkl_hip_poseidon_permute (both permutation forms) vs the oracle permutation, on
+    random states, a partial last batch and the extreme elements 0, 1, p-1, 2^127."""
+    rng = random.Random(11 + engine)
+    P = oracle.P
+    n = 1000
+    edge = [0, 1, P - 1, 1 << 127, P - 2, (1 << 64) - 1, 1 << 64]
+    states = [[e] * 12 for e in edge] + [[rng.choice(edge) for _ in range(12)] for _ in range(9)]
+    states += [[rng.randrange(P) for _ in range(12)] for _ in range(n - len(states))]
+    flat = [x for s in states for x in s]
+    d = gpu_ctx.alloc(16 * len(flat))
+    gpu_ctx.upload(d, _fe_buf(flat), 16 * len(flat))
+    gpu_ctx.poseidon_permute(d, n, engine)
+    got = gpu_ctx.download(d, 16 * len(flat))
+    gpu_ctx.free(d)
+    for i in list(range(40)) + list(range(40, n, 37)) + [n - 1]:
+        want = oracle.permute(states[i])
+        have = [int.from_bytes(got[16 * (12 * i + j):16 * (12 * i + j) + 16], "little") for j in range(12)]
+        assert have == want, f"state {i}"
+
+
+def _row_digest(oracle, row, np_, rate=16):
+    ncols = len(row)
+    psize = ncols
+    if np_ > 1:
+        psize = max(-(-ncols // np_), rate)
+    if psize == ncols:
+        return oracle.hash_elements(row)
+    return oracle.merge_many([oracle.hash_elements(row[c:c + psize]) for c in range(0, ncols, psize)])
+
+
+@pytest.mark.parametrize("ncols,nrows,np_", [
+    (51, 1000, 1),     # one partition, partial last batch of 32 rows
+    (204, 1056, 4),    # trace commitment shape (4 x 51 + merge_many)
+    (256, 544, 16),    # 16 partitions: merge_many absorbs over two blocks
+    (7, 2048, 4),      # composition shape (one 16-wide partition + merge_many)
+    (33, 96, 2),
+])
+def test_stage_hash_rows_matrix_core(oracle, gpu_ctx, pm_policy, ncols, nrows, np_):
+    rng = random.Random(ncols * 7 + nrows)
+    P = oracle.P
+    vals = [rng.randrange(P) for _ in range(ncols * nrows)]
+    raw = _fe_buf(vals)
+    d_m = gpu_ctx.alloc(len(raw))
+    d_o = gpu_ctx.alloc(nrows * 16)
+    d_nodes = gpu_ctx.alloc(2 * 1024 * 16)
+    gpu_ctx.upload(d_m, raw, len(raw))
+    gpu_ctx.hash_rows(d_m, ncols, nrows, np_, 16, d_o)
+    got = gpu_ctx.download(d_o, nrows * 16)
+    for r in sorted(set(list(range(0, nrows, 53)) + [nrows - 1, 31, 32])):
+        row = [vals[c * nrows + r] for c in range(ncols)]
+        assert int.from_bytes(got[16 * r:16 * r + 16], "little") == _row_digest(oracle, row, np_), f"row {r}"
+    if nrows >= 1024:  # Merkle tree over the first 1024 digests (levels of 512..32 on the matrix cores)
+        gpu_ctx.merkle_tree(d_o, 1024, d_nodes)
+        nodes = gpu_ctx.download(d_nodes, 2 * 1024 * 16)
+        lvl = [int.from_bytes(got[16 * i:16 * i + 16], "little") for i in range(1024)]
+        while len(lvl) > 1:
+            lvl = [oracle.merge(lvl[2 * i], lvl[2 * i + 1]) for i in range(len(lvl) // 2)]
+        assert int.from_bytes(nodes[16:32], "little") == lvl[0]
+    for d in (d_m, d_o, d_nodes):
+        gpu_ctx.free(d)
+
+
+@pytest.mark.parametrize("log_n,q,blowup,grind,flags", [
+    (6, 32, 16, 4, 0), (8, 64, 16, 8, 0), (7, 40, 8, 2, 1), (6, 16, 16, 2, 2),
+])
+def test_proof_bytes_match_oracle_matrix_core(oracle, gpu_ctx, pm_policy, log_n, q, blowup, grind, flags):
+    """Every commitment level of >= 32 states (trace/composition rows, Merkle levels, FRI
+    leaves) on the matrix-core permutation: proof bytes still equal the oracle's."""
+    import zkl_hip
+    n = 1 << log_n
+    seed = 0x3C0DE00 + log_n + 16 * flags
+    t, pi, w = zkl_hip.synth_vm_segment(seed, log_n, flags)
+    opts = zkl_hip.proof_options(w, n, queries=q, blowup=blowup, grind=grind)
+    got = gpu_ctx.prove_segment(t, w, n, pi, opts)
+    ot, opi, _ = oracle.synth_segment(seed, log_n, flags)
+    oo = oracle.ProofOptions(*[getattr(opts, f) for f, _ in opts._fields_])
+    want = oracle.prove(ot, w, n, opi, oo)
+    assert got == want

@@ -59,6 +59,14 @@ def main():
     ms = timeit(lambda: ctx.merkle_tree(d_out, n, d_nodes))
     out["tree_ms"] = round(ms, 3)
     out["tree_Mperm_s"] = round((n - 1) / ms / 1e3, 1)
+    # raw permutations (2^log_rows states) in both forms
+    d_st = ctx.alloc(n * 12 * 16)
+    ctx.upload(d_st, host.ctypes.data, n * 12 * 16)
+    for eng, name in ((1, "perm_mfma"), (0, "perm_lane")):
+        ms = timeit(lambda: ctx.poseidon_permute(d_st, n, eng))
+        out[name + "_ms"] = round(ms, 3)
+        out[name + "_Mperm_s"] = round(n / ms / 1e3, 1)
+    ctx.free(d_st)
     # NTT: W columns of 2^log_rows, DIT (bit-reversed -> natural), all stages (3 passes at 2^20)
     ms = timeit(lambda: ctx.ntt(d_mat, W, n, dif=False))
     out["ntt_dit_ms"] = round(ms, 3)

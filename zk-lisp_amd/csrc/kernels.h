@@ -25,6 +25,13 @@ struct HasherMont {
 };
 HasherMont make_hasher_mont(const HasherConsts& h);
 void upload_hasher_mont(const HasherMont& m, hipStream_t s);
+// matrix-core permutation tables (A digits of the MDS, round constants), built once
+void upload_pm_tables(const HasherConsts& h, hipStream_t s);
+// 1 = matrix-core permutation on throughput-bound levels (default), 0 = lane groups only
+int hash_engine();
+void set_hash_policy(int engine, size_t min_items);
+// n Poseidon permutations of 12-element canonical states in place (engine as above)
+void launch_permute(fe* d_states, size_t n, int engine, hipStream_t s);
 struct CeParams;
 struct ProofConsts;  // per-proof constants in device memory, one block per context (below)
 void upload_air_consts(ProofConsts* dK, const AirDevice& a, hipStream_t s);

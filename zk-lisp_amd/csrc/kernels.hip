@@ -7,6 +7,12 @@
 // computing the same residues, independent of evaluation order.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
 #include <vector>
 
 #include "kernels.h"
@@ -413,6 +419,8 @@ static inline unsigned pg_blocks(size_t items) {
   return (unsigned)((items + per - 1) / per);
 }
 
+#include "poseidon_mfma.inc"
+
 // ---- row hashing (Winterfell partitioned row hash): one group per row.  The row's
 // partitions are hashed one after another (hash_elements over psize columns, chunked in
 // folded pairs); with more than one partition their digests are merged with merge_many.
@@ -482,6 +490,14 @@ void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np
     psize = (ncols + np - 1) / np;
     if (psize < rate) psize = rate;  // PartitionOptions::partition_size, ExtensionDegree 1
   }
+  const uint32_t np_eff = (ncols + psize - 1) / psize;
+  if (hash_engine() == 1 && nrows >= pm_min_items() && np_eff <= (uint32_t)PM_MAX_PARTS) {
+    if (tag == 1)
+      hash_rows_pm_kernel<1><<<pm_grid(nrows), PM_THREADS, 0, s>>>(d_mat, ncols, nrows, psize, d_out);
+    else
+      hash_rows_pm_kernel<0><<<pm_grid(nrows), PM_THREADS, 0, s>>>(d_mat, ncols, nrows, psize, d_out);
+    return;
+  }
   if (tag == 1)
     hash_rows_kernel<1><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, d_out);
   else
@@ -500,6 +516,8 @@ void launch_merkle(fe* d_nodes, size_t n, hipStream_t s) {
   for (size_t lvl = n / 2; lvl >= 1; lvl /= 2) {
     if (lvl <= PW_MAX_ITEMS)
       merkle_level_wide_kernel<<<pw_blocks(lvl), 256, 0, s>>>(d_nodes, lvl);
+    else if (hash_engine() == 1 && lvl >= pm_min_items())
+      merkle_level_pm_kernel<<<pm_grid(lvl), PM_THREADS, 0, s>>>(d_nodes, lvl);
     else
       merkle_level_kernel<<<pg_blocks(lvl), 256, 0, s>>>(d_nodes, lvl);
   }
@@ -525,6 +543,24 @@ __global__ __launch_bounds__(64) void fri_coin_kernel(fe* coin, const fe* root, 
 }
 void launch_fri_coin(fe* d_coin, const fe* d_root, fe* d_root_out, hipStream_t s) {
   fri_coin_kernel<<<1, 64, 0, s>>>(d_coin, d_root, d_root_out);
+}
+
+__global__ PG_KERNEL void pg_permute_kernel(fe* st, size_t n) {
+  PG_SETUP();
+  const bool live = P.g < PG_PER_WAVE && item < n;
+  const size_t i = live ? item : 0;
+  uint32_t x[5];
+  to_mont(st[i * 12 + P.j], x);
+  pg_permute(P, x);
+  if (live) st[i * 12 + P.j] = from_mont(x);
+}
+
+void launch_permute(fe* d_states, size_t n, int engine, hipStream_t s) {
+  if (!n) return;
+  if (engine == 1)
+    pm_permute_kernel<<<pm_grid(n), PM_THREADS, 0, s>>>(d_states, n);
+  else
+    pg_permute_kernel<<<pg_blocks(n), 256, 0, s>>>(d_states, n);
 }
 
 void launch_draws(fe seed, uint64_t base, size_t k, fe* d_out, hipStream_t s) {
@@ -1239,6 +1275,8 @@ void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s) {
   size_t h = Nd / 2;
   if (h <= PW_MAX_ITEMS)
     fri_leaf_wide_kernel<<<pw_blocks(h), 256, 0, s>>>(d_ev, h, d_leaves);
+  else if (hash_engine() == 1 && h >= pm_min_items())
+    fri_leaf_pm_kernel<<<pm_grid(h), PM_THREADS, 0, s>>>(d_ev, h, d_leaves);
   else
     fri_leaf_kernel<<<pg_blocks(h), 256, 0, s>>>(d_ev, h, d_leaves);
 }

@@ -197,6 +197,7 @@ void upload_hasher(hipStream_t s) {
     hm = make_hasher_mont(hc);
   });
   upload_hasher_mont(hm, s);
+  upload_pm_tables(hc, s);
 }
 
 void ensure_tables(zkl_ctx* C, size_t n, size_t N) {
@@ -891,6 +892,23 @@ int zkl_hip_hash_rows(zkl_ctx* c, const void* d_m, uint32_t nc, uint32_t nr, uin
     upload_hasher(c->stream);
     c->parts.ensure((size_t)std::max<uint32_t>(np, 1) * nr * sizeof(fe) + 16);
     launch_hash_rows((const fe*)d_m, nc, nr, np, rate, c->parts.f(), (fe*)d_out, c->stream);
+    HIPCHECK(hipStreamSynchronize(c->stream));
+  });
+}
+
+int zkl_hip_set_hash_policy(int engine, uint32_t pm_min_items) {
+  if (engine < 0 || engine > 1) return ZKL_E_INVALID;
+  set_hash_policy(engine, pm_min_items);
+  return 0;
+}
+
+int zkl_hip_poseidon_permute(zkl_ctx* c, void* d_states, uint32_t n_states, int engine) {
+  if (!c || !d_states || engine < 0 || engine > 1) return ZKL_E_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  return run_guarded(c, [&] {
+    HIPCHECK(hipSetDevice(c->device));
+    upload_hasher(c->stream);
+    launch_permute((fe*)d_states, n_states, engine, c->stream);
     HIPCHECK(hipStreamSynchronize(c->stream));
   });
 }

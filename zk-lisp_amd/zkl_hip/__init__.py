@@ -111,6 +111,8 @@ def load_library():
     lib.zkl_hip_ntt.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int]
     lib.zkl_hip_hash_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]
     lib.zkl_hip_merkle_tree.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
+    lib.zkl_hip_poseidon_permute.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int]
+    lib.zkl_hip_set_hash_policy.argtypes = [C.c_int, C.c_uint32]
     lib.zkl_hip_lde.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]
     _lib = lib
     return lib
@@ -254,6 +256,11 @@ class Context:
     def hash_rows(self, d_mat, n_cols, n_rows, num_partitions, hash_rate, d_out):
         rc = self.lib.zkl_hip_hash_rows(self.ptr, C.c_void_p(d_mat), n_cols, n_rows, num_partitions, hash_rate,
                                         C.c_void_p(d_out))
+        if rc:
+            self._err(rc)
+
+    def poseidon_permute(self, d_states, n_states, engine=1):
+        rc = self.lib.zkl_hip_poseidon_permute(self.ptr, C.c_void_p(d_states), n_states, engine)
         if rc:
             self._err(rc)
 
