@@ -30,9 +30,12 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # counts one quad-cycle per instruction for this kernel's 64-bit integer mix), 256 CUs x 4
 # SIMDs x 2.4 GHz / 4
 VALU_ISSUE_PEAK_G = 256 * 4 * 2.4 / 4   # G wave-instructions/s
-# VALU wave-instructions per Poseidon permutation of the lane-group kernel, from
-# SQ_INSTS_VALU / permutations (profiles/r01/pmc_sq_stagebench.json)
-VALU_INSTR_PER_PERM = 2617
+# VALU wave-instructions per Poseidon permutation of the trace row hash, from
+# SQ_INSTS_VALU / permutations: matrix-core kernel hash_rows_pm_kernel<0> 1025
+# (profiles/r01/pmc_sq_pm.json; the MDS runs on v_mfma_i32_32x32x32_i8), lane-group kernel
+# hash_rows_kernel<0> 2617 (profiles/r01/pmc_sq_stagebench.json, ZKL_HASH_ENGINE=lane)
+VALU_INSTR_PER_PERM = {"mfma": 1025, "lane": 2617}
+ROW_KERNEL = {"mfma": "hash_rows_pm_kernel<0>", "lane": "hash_rows_kernel<0>"}
 
 
 def log(*a):
@@ -219,8 +222,10 @@ def main():
         pm = perm_model(n)
         perms_per_launch = N * pm["row_perms"]  # fused: partitions + merge_many per row
         perms_per_s = perms_per_launch / (per_launch_ms * 1e-3)
-        valu_g = perms_per_s * VALU_INSTR_PER_PERM / 1e9
-        traffic = load_traffic("hash_rows_kernel<0>")
+        engine = "lane" if os.environ.get("ZKL_HASH_ENGINE") == "lane" else "mfma"
+        kname = ROW_KERNEL[engine]
+        valu_g = perms_per_s * VALU_INSTR_PER_PERM[engine] / 1e9
+        traffic = load_traffic(kname)
         out = {
             "metric": METRIC,
             "value": round(value, 4),
@@ -243,7 +248,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "hash_rows_kernel<0> (trace LDE row hashing, 4 partitions + merge_many)",
+                "kernel": f"{kname} (trace LDE row hashing, 4 partitions + merge_many)",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -255,7 +260,7 @@ def main():
             },
             "roofline_valu": {
                 "bound": "valu-issue",
-                "kernel": "hash_rows_kernel<0>",
+                "kernel": kname,
                 "achieved": round(valu_g, 1),
                 "peak": VALU_ISSUE_PEAK_G,
                 "unit": "G VALU wave-instructions/s",
@@ -263,7 +268,8 @@ def main():
                 "perms_per_launch": perms_per_launch,
                 "perms_per_s": round(perms_per_s),
                 "f128_mulmods_per_s": round(perms_per_s * MULMODS_PER_PERM),
-                "note": "SQ counters show ~98% VALU issue occupancy per SIMD (profiles/r01/pmc_sq_stagebench.json)",
+                "note": "VALU wave-instructions per permutation from SQ_INSTS_VALU (profiles/r01/pmc_sq_pm.json); "
+                        "the 12x12 MDS runs on the matrix cores (MFMA busy ~21% of cycles)",
             },
             "dominant_kernel_family": dom,
             "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kacc.items()},

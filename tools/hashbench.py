@@ -25,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--log-rows", type=int, default=20)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--only", default="", help="comma list of: rows,comp,tree,perm,ntt (default all)")
     args = ap.parse_args()
     import numpy as np
     import zkl_hip
@@ -49,28 +50,33 @@ def main():
         return (time.perf_counter() - t0) / args.reps * 1e3
 
     out = {"lib": os.environ.get("ZKL_HIP_LIB", "default"), "rows": n}
-    ms = timeit(lambda: ctx.hash_rows(d_mat, W, n, 4, 16, d_out))
-    perms = n * (4 * 3 + 1)
-    out["rows_ms"] = round(ms, 3)
-    out["rows_Mperm_s"] = round(perms / ms / 1e3, 1)
-    ms = timeit(lambda: ctx.hash_rows(d_mat, 7, n, 4, 16, d_out))
-    out["comp_ms"] = round(ms, 3)
-    out["comp_Mperm_s"] = round(2 * n / ms / 1e3, 1)
-    ms = timeit(lambda: ctx.merkle_tree(d_out, n, d_nodes))
-    out["tree_ms"] = round(ms, 3)
-    out["tree_Mperm_s"] = round((n - 1) / ms / 1e3, 1)
+    only = set(args.only.split(",")) if args.only else {"rows", "comp", "tree", "perm", "ntt"}
+    if "rows" in only:
+        ms = timeit(lambda: ctx.hash_rows(d_mat, W, n, 4, 16, d_out))
+        perms = n * (4 * 3 + 1)
+        out["rows_ms"] = round(ms, 3)
+        out["rows_Mperm_s"] = round(perms / ms / 1e3, 1)
+    if "comp" in only:
+        ms = timeit(lambda: ctx.hash_rows(d_mat, 7, n, 4, 16, d_out))
+        out["comp_ms"] = round(ms, 3)
+        out["comp_Mperm_s"] = round(2 * n / ms / 1e3, 1)
+    if "tree" in only:
+        ms = timeit(lambda: ctx.merkle_tree(d_out, n, d_nodes))
+        out["tree_ms"] = round(ms, 3)
+        out["tree_Mperm_s"] = round((n - 1) / ms / 1e3, 1)
     # raw permutations (2^log_rows states) in both forms
-    d_st = ctx.alloc(n * 12 * 16)
-    ctx.upload(d_st, host.ctypes.data, n * 12 * 16)
-    for eng, name in ((1, "perm_mfma"), (0, "perm_lane")):
-        ms = timeit(lambda: ctx.poseidon_permute(d_st, n, eng))
-        out[name + "_ms"] = round(ms, 3)
-        out[name + "_Mperm_s"] = round(n / ms / 1e3, 1)
-    ctx.free(d_st)
-    # NTT: W columns of 2^log_rows, DIT (bit-reversed -> natural), all stages (3 passes at 2^20)
-    ms = timeit(lambda: ctx.ntt(d_mat, W, n, dif=False))
-    out["ntt_dit_ms"] = round(ms, 3)
-    out["ntt_Gbfly_s"] = round(W * (n // 2) * args.log_rows / ms / 1e6, 1)
+    if "perm" in only:
+        d_st = ctx.alloc(n * 12 * 16)
+        ctx.upload(d_st, host.ctypes.data, n * 12 * 16)
+        for eng, name in ((1, "perm_mfma"), (0, "perm_lane")):
+            ms = timeit(lambda: ctx.poseidon_permute(d_st, n, eng))
+            out[name + "_ms"] = round(ms, 3)
+            out[name + "_Mperm_s"] = round(n / ms / 1e3, 1)
+        ctx.free(d_st)
+    if "ntt" in only:  # W columns of 2^log_rows, DIT (bit-reversed -> natural), all stages
+        ms = timeit(lambda: ctx.ntt(d_mat, W, n, dif=False))
+        out["ntt_dit_ms"] = round(ms, 3)
+        out["ntt_Gbfly_s"] = round(W * (n // 2) * args.log_rows / ms / 1e6, 1)
     print(json.dumps(out), flush=True)
     for p in (d_mat, d_out, d_nodes):
         ctx.free(p)
