@@ -87,6 +87,32 @@ typedef struct {
   uint32_t ram_delta_clk_bits;
 } zkl_air_public_inputs;
 
+/* ---- zl1 step proof (a18) --------------------------------------------------------
+ * zk_lisp_proof::pi::VmArg (pi.rs) for the ZKLSTP1 encoding: tag 0 = U64 (bytes[0..8] LE),
+ * 1 = U128 (bytes[0..16] LE), 2 = Bytes32. */
+typedef struct {
+  uint32_t tag;
+  uint8_t bytes[32];
+} zkl_vm_arg;
+
+/* What prove_segment (prove.rs:1057-1175) feeds Proof::new_multi_segment (format.rs:105-148)
+ * and StepProof besides the inner proof and the AirPublicInputs: the suite id (= program_id,
+ * prove.rs:985), the security target echoed as lambda (opts.min_security_bits, prove.rs:634),
+ * the segment position, the VM state hashes from the trace builder and the
+ * SegmentBoundaryBytes (prove.rs:1112), and the typed main_args of the core public inputs. */
+typedef struct {
+  uint8_t suite_id[32];
+  uint32_t lambda_bits;
+  uint32_t segment_index, segments_total;
+  uint8_t pc_init[32];
+  uint8_t state_in_hash[32], state_out_hash[32];
+  uint8_t ram_gp_unsorted_in[32], ram_gp_unsorted_out[32], ram_gp_sorted_in[32], ram_gp_sorted_out[32];
+  uint8_t rom_s_in[3][32];
+  uint8_t rom_s_out[3][32];
+  uint32_t n_main_args;
+  zkl_vm_arg main_args[ZKL_MAX_MAIN_SLOTS];
+} zkl_step_info;
+
 /* Per-stage wall times of the last proof on a ctx, milliseconds; stage names follow
  * the reference's tracing events (prove.rs:464-513): trace_lde, trace_commit,
  * coefficients, evaluator, constraint_commitment, ood, deep, fri, grind, queries. */
@@ -128,6 +154,9 @@ int zkl_hip_stage_times(const zkl_ctx* ctx, double* out_ms, int max_n);
  * *names receives a static '\n'-separated list of the family names. */
 #define ZKL_NUM_KFAMILIES 9
 int zkl_hip_kernel_times(const zkl_ctx* ctx, double* out_ms, int* out_launches, int max_n, const char** names);
+/* Which kernel families zkl_hip_kernel_times covers for the following proofs: 0 none,
+ * 1 the trace row hash only (default: every bracket costs ~10 us of queue time), 2 all. */
+int zkl_hip_set_kernel_timing(zkl_ctx* ctx, int mode);
 
 /* ---- device memory (the library's own HIP runtime; callers need no torch) --- */
 int zkl_hip_device_count(int* count);
@@ -156,7 +185,7 @@ int zkl_hip_merkle_tree(zkl_ctx* ctx, const void* d_leaves, uint32_t n_leaves, v
  * use on large levels), 0 = lane-group form.  Stage entry point for parity tests. */
 int zkl_hip_poseidon_permute(zkl_ctx* ctx, void* d_states, uint32_t n_states, int engine);
 /* Process-wide hashing policy: engine 1 (default) runs Poseidon levels of at least
- * pm_min_items states (default 65536) on the matrix-core permutation, engine 0 keeps every
+ * pm_min_items states (default 16384) on the matrix-core permutation, engine 0 keeps every
  * level on lane groups.  Both give identical digests; this only moves time. */
 int zkl_hip_set_hash_policy(int engine, uint32_t pm_min_items);
 /* Coset low-degree extension of column-major n_cols x n_rows evaluations over
@@ -192,6 +221,21 @@ int zkl_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128* trace_out,
 #define ZKL_SYN_MERKLE 4u
 int zkl_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f128* trace_out,
                             zkl_air_public_inputs* pi_out, uint32_t* width_out);
+
+/* ---- zl1 step proof (host-side, no device work) ----------------------------------
+ * StepProof::to_bytes (proof/step.rs:79-151) of the step proof prove_segment builds around
+ * an inner proof from zkl_hip_prove_segment*: "ZKLSTP1" | lambda | suite | core pi |
+ * main_args | vm_usage_mask | ram_delta_clk_bits | rom_acc | segment index/total | pc_init |
+ * state hashes | boundary bytes | inner proof (length-prefixed).  Buffer released with
+ * zkl_hip_free. */
+int zkl_step_proof_encode(const zkl_air_public_inputs* pi, const zkl_step_info* info, const uint8_t* inner,
+                          size_t inner_len, uint8_t** out, size_t* out_len);
+/* Decode a ZKLSTP1 encoding (StepProof::from_bytes, step.rs:153-493) and return the zl1
+ * commitment echo root_trace = BLAKE3("zkl/step/root_trace" | suite | trace roots |
+ * constraint root | FRI roots) (format.rs:214-238) and the step digest
+ * (proof/digest.rs:16-68).  Either output may be NULL.  Errors: ZKL_E_INVALID with
+ * zkl_hip_last_error(NULL) naming the truncated/invalid field, as step.rs does. */
+int zkl_step_proof_digest(const uint8_t* step, size_t len, uint8_t digest_out[32], uint8_t root_trace_out[32]);
 
 #ifdef __cplusplus
 }

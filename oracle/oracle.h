@@ -127,4 +127,9 @@ int orc_verify_segment(const uint8_t *proof, size_t len, const zkl_air_public_in
                        const zkl_proof_options *opts, char *err, size_t errlen);
 void orc_free(void *p);
 
+/* ---------------- zl1 step proof (proof/step.rs, format.rs, digest.rs) ---------------- */
+int orc_step_encode(const zkl_air_public_inputs *pi, const zkl_step_info *s, const uint8_t *inner, size_t inner_len,
+                    uint8_t **out, size_t *out_len);
+int orc_step_digest(const uint8_t *p, size_t n, uint8_t digest[32], uint8_t rt[32], char *err, size_t errlen);
+
 #endif

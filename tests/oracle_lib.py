@@ -231,3 +231,25 @@ def last_times():
     arr = (C.c_double * 8)()
     lib().orc_last_times(arr)
     return list(arr)
+
+
+def step_encode(pi, info, inner: bytes) -> bytes:
+    """oracle/step.c: StepProof::to_bytes restatement (info: zkl_hip.StepInfo layout)."""
+    out = C.POINTER(C.c_uint8)()
+    ln = C.c_size_t()
+    rc = lib().orc_step_encode(C.byref(pi), C.byref(info), inner, C.c_size_t(len(inner)), C.byref(out), C.byref(ln))
+    if rc != 0:
+        raise ValueError("oracle step encode failed")
+    data = bytes(out[:ln.value])
+    lib().orc_free(out)
+    return data
+
+
+def step_digest(step: bytes):
+    """oracle/step.c: (digest, root_trace) or raises ValueError(message)."""
+    d, r = (C.c_uint8 * 32)(), (C.c_uint8 * 32)()
+    err = C.create_string_buffer(256)
+    rc = lib().orc_step_digest(step, C.c_size_t(len(step)), d, r, err, C.c_size_t(256))
+    if rc != 0:
+        raise ValueError(err.value.decode())
+    return bytes(d), bytes(r)

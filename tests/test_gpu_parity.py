@@ -379,7 +379,7 @@ def pm_policy(gpu_ctx):
     lib = zkl_hip.load_library()
     assert lib.zkl_hip_set_hash_policy(1, 32) == 0
     yield
-    assert lib.zkl_hip_set_hash_policy(1, 1 << 16) == 0
+    assert lib.zkl_hip_set_hash_policy(1, 1 << 14) == 0
 
 
 def _fe_buf(vals):
@@ -466,3 +466,23 @@ def test_proof_bytes_match_oracle_matrix_core(oracle, gpu_ctx, pm_policy, log_n,
     oo = oracle.ProofOptions(*[getattr(opts, f) for f, _ in opts._fields_])
     want = oracle.prove(ot, w, n, opi, oo)
     assert got == want
+
+
+def test_step_proof_of_gpu_proof(oracle, gpu_ctx):
+    """zl1 step proof (a18) around a GPU inner proof: the ZKLSTP1 bytes, root_trace and step
+    digest equal the oracle's around the oracle's proof of the same segment."""
+    import zkl_hip
+    n = 1 << 7
+    t, pi, w = zkl_hip.synth_vm_segment(0x57E9A007, 7)
+    opts = zkl_hip.proof_options(w, n, queries=16, grind=4)
+    inner = gpu_ctx.prove_segment(t, w, n, pi, opts)
+    info = zkl_hip.StepInfo()
+    info.suite_id[:] = bytes(pi.program_id)
+    info.lambda_bits, info.segment_index, info.segments_total = 96, 3, 8
+    info.state_in_hash[:] = bytes(range(32))
+    step = zkl_hip.step_proof_encode(pi, info, inner)
+    ot, opi, _ = oracle.synth_segment(0x57E9A007, 7)
+    oo = oracle.ProofOptions(*[getattr(opts, f) for f, _ in opts._fields_])
+    want = oracle.step_encode(opi, info, oracle.prove(ot, w, n, opi, oo))
+    assert step == want
+    assert zkl_hip.step_proof_digest(step) == oracle.step_digest(want)

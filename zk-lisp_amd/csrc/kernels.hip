@@ -493,9 +493,9 @@ void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np
   const uint32_t np_eff = (ncols + psize - 1) / psize;
   if (hash_engine() == 1 && nrows >= pm_min_items() && np_eff <= (uint32_t)PM_MAX_PARTS) {
     if (tag == 1)
-      hash_rows_pm_kernel<1><<<pm_grid(nrows), PM_THREADS, 0, s>>>(d_mat, ncols, nrows, psize, d_out);
+      PM_GO(hash_rows_pm_kernel<1>, nrows, true, s)(d_mat, ncols, nrows, psize, d_out);
     else
-      hash_rows_pm_kernel<0><<<pm_grid(nrows), PM_THREADS, 0, s>>>(d_mat, ncols, nrows, psize, d_out);
+      PM_GO(hash_rows_pm_kernel<0>, nrows, true, s)(d_mat, ncols, nrows, psize, d_out);
     return;
   }
   if (tag == 1)
@@ -512,14 +512,44 @@ __global__ __launch_bounds__(256) void merkle_level_wide_kernel(fe* nodes, size_
   if (live && P.e == 0 && P.h == 0) nodes[i] = d;
 }
 
+// Tree top: several levels per launch.  Workgroup g (4 waves, 8 wide groups, one wave per
+// SIMD) owns nodes [cnt*g, cnt*g + cnt) of level lvl and reduces them to one node of level
+// lvl/cnt, with a workgroup barrier between levels; waves without a live node skip the
+// permutation.  A launch per level would add ~10 us of dispatch latency to each of these
+// permutation-latency-bound levels.
+constexpr int TOP_WAVES = 4;
+constexpr int TOP_SLOTS = TOP_WAVES * PW_PER_WAVE;  // 8
+__global__ __launch_bounds__(64 * TOP_WAVES) void merkle_top_kernel(fe* nodes, size_t lvl, int cnt) {
+  __shared__ __align__(16) uint32_t pw_lds[TOP_WAVES * PW_WAVE_WORDS];
+  PWGroup P;
+  pw_init(P, pw_lds);
+  const int wave_slot0 = (int)(threadIdx.x >> 6) * PW_PER_WAVE;
+  const int slot = wave_slot0 + P.g;
+  size_t L = lvl, base = (size_t)blockIdx.x * cnt;
+  for (int c = cnt; c >= 1; c >>= 1, L >>= 1, base >>= 1) {
+    if (wave_slot0 < c) {  // wave-uniform
+      const bool live = P.g < PW_PER_WAVE && slot < c;
+      const size_t i = L + base + (live ? slot : 0);
+      fe d = pw_sponge<DOM_MERGE>(P, live, 2, [&](int j) { return nodes[2 * i + j]; });
+      if (live && P.e == 0 && P.h == 0) nodes[i] = d;
+    }
+    __syncthreads();
+  }
+}
+
 void launch_merkle(fe* d_nodes, size_t n, hipStream_t s) {
-  for (size_t lvl = n / 2; lvl >= 1; lvl /= 2) {
-    if (lvl <= PW_MAX_ITEMS)
-      merkle_level_wide_kernel<<<pw_blocks(lvl), 256, 0, s>>>(d_nodes, lvl);
-    else if (hash_engine() == 1 && lvl >= pm_min_items())
-      merkle_level_pm_kernel<<<pm_grid(lvl), PM_THREADS, 0, s>>>(d_nodes, lvl);
+  for (size_t lvl = n / 2; lvl >= 1;) {
+    if (lvl <= PW_MAX_ITEMS) {
+      const size_t cnt = std::min<size_t>(lvl, TOP_SLOTS);
+      merkle_top_kernel<<<(unsigned)(lvl / cnt), 64 * TOP_WAVES, 0, s>>>(d_nodes, lvl, (int)cnt);
+      lvl /= cnt * 2;
+      continue;
+    }
+    if (hash_engine() == 1 && lvl >= pm_min_items())
+      PM_GO(merkle_level_pm_kernel, lvl, false, s)(d_nodes, lvl);
     else
       merkle_level_kernel<<<pg_blocks(lvl), 256, 0, s>>>(d_nodes, lvl);
+    lvl /= 2;
   }
 }
 
@@ -558,17 +588,24 @@ __global__ PG_KERNEL void pg_permute_kernel(fe* st, size_t n) {
 void launch_permute(fe* d_states, size_t n, int engine, hipStream_t s) {
   if (!n) return;
   if (engine == 1)
-    pm_permute_kernel<<<pm_grid(n), PM_THREADS, 0, s>>>(d_states, n);
+    PM_GO(pm_permute_kernel, n, false, s)(d_states, n);
   else
     pg_permute_kernel<<<pg_blocks(n), 256, 0, s>>>(d_states, n);
 }
 
 void launch_draws(fe seed, uint64_t base, size_t k, fe* d_out, hipStream_t s) {
-  if (k) draw_kernel<<<pg_blocks(k), 256, 0, s>>>(seed, base, k, d_out);
+  if (!k) return;
+  if (hash_engine() == 1 && k >= pm_min_items())
+    PM_GO(draw_pm_kernel, k, false, s)(seed, base, k, d_out);
+  else
+    draw_kernel<<<pg_blocks(k), 256, 0, s>>>(seed, base, k, d_out);
 }
 
 void launch_grind(fe seed, uint64_t base, uint32_t count, uint32_t bits, unsigned long long* d_best, hipStream_t s) {
-  grind_kernel<<<pg_blocks(count), 256, 0, s>>>(seed, base, count, bits, d_best);
+  if (hash_engine() == 1 && count >= pm_min_items())
+    PM_GO(grind_pm_kernel, count, false, s)(seed, base, count, bits, d_best);
+  else
+    grind_kernel<<<pg_blocks(count), 256, 0, s>>>(seed, base, count, bits, d_best);
 }
 
 // =====================================================================================
@@ -1276,7 +1313,7 @@ void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s) {
   if (h <= PW_MAX_ITEMS)
     fri_leaf_wide_kernel<<<pw_blocks(h), 256, 0, s>>>(d_ev, h, d_leaves);
   else if (hash_engine() == 1 && h >= pm_min_items())
-    fri_leaf_pm_kernel<<<pm_grid(h), PM_THREADS, 0, s>>>(d_ev, h, d_leaves);
+    PM_GO(fri_leaf_pm_kernel, h, false, s)(d_ev, h, d_leaves);
   else
     fri_leaf_kernel<<<pg_blocks(h), 256, 0, s>>>(d_ev, h, d_leaves);
 }

@@ -24,6 +24,12 @@
 
 using namespace zkl;
 
+namespace zkl {  // step.cpp
+std::vector<uint8_t> step_encode(const zkl_air_public_inputs& pi, const zkl_step_info& s, const uint8_t* inner,
+                                 size_t inner_len);
+void step_digest(const uint8_t* p, size_t n, uint8_t digest[32], uint8_t rt[32]);
+}  // namespace zkl
+
 namespace {
 
 #define HIPCHECK(x)                                                                           \
@@ -135,6 +141,7 @@ struct zkl_ctx {
   std::vector<hipEvent_t> evpool;
   std::vector<std::pair<int, size_t>> kmarks;  // (family, index of start event; stop = +1)
   size_t evnext = 0;
+  int ktiming = 1;  // 0: no kernel-family events, 1: trace row hash only, 2: every family
   double kfam_ms[ZKL_NUM_KFAMILIES] = {0};
   int kfam_n[ZKL_NUM_KFAMILIES] = {0};
 };
@@ -148,7 +155,11 @@ namespace {
 struct KScope {
   zkl_ctx* C;
   size_t i;
-  KScope(zkl_ctx* c, int fam) : C(c) {
+  // Each event record costs ~10 us of queue time between kernels, so by default only the
+  // dominant family (the trace row hash) is bracketed; zkl_hip_set_kernel_timing(ctx, 2)
+  // times every family (breakdown runs outside the timed region).
+  KScope(zkl_ctx* c, int fam) : C(c), i(SIZE_MAX) {
+    if (!(C->ktiming == 2 || (C->ktiming == 1 && fam == KF_TRACE_HASH))) return;
     if (C->evnext + 2 > C->evpool.size()) {
       size_t old = C->evpool.size();
       C->evpool.resize(old + 256);
@@ -159,7 +170,9 @@ struct KScope {
     C->kmarks.push_back({fam, i});
     (void)hipEventRecord(C->evpool[i], C->stream);
   }
-  ~KScope() { (void)hipEventRecord(C->evpool[i + 1], C->stream); }
+  ~KScope() {
+    if (i != SIZE_MAX) (void)hipEventRecord(C->evpool[i + 1], C->stream);
+  }
 };
 
 void resolve_kernel_times(zkl_ctx* C) {
@@ -730,6 +743,9 @@ int run_guarded(zkl_ctx* ctx, const std::function<void()>& f) {
   } catch (const InvalidArg& e) {
     set_err(ctx, e.what());
     return ZKL_E_INVALID;
+  } catch (const std::invalid_argument& e) {
+    set_err(ctx, e.what());
+    return ZKL_E_INVALID;
   } catch (const DeviceError& e) {
     set_err(ctx, e.what());
     return ZKL_E_DEVICE;
@@ -834,6 +850,27 @@ int zkl_hip_kernel_times(const zkl_ctx* c, double* out, int* launches, int max_n
     if (launches) launches[i] = c->kfam_n[i];
   }
   return k;
+}
+
+int zkl_hip_set_kernel_timing(zkl_ctx* c, int mode) {
+  if (!c || mode < 0 || mode > 2) return ZKL_E_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->ktiming = mode;
+  return 0;
+}
+
+int zkl_step_proof_encode(const zkl_air_public_inputs* pi, const zkl_step_info* info, const uint8_t* inner,
+                          size_t inner_len, uint8_t** out, size_t* out_len) {
+  if (!pi || !info || !inner || !out || !out_len) return ZKL_E_INVALID;
+  std::vector<uint8_t> v;
+  int rc = run_guarded(nullptr, [&] { v = step_encode(*pi, *info, inner, inner_len); });
+  if (rc) return rc;
+  return finish_proof(v, out, out_len);
+}
+
+int zkl_step_proof_digest(const uint8_t* step, size_t len, uint8_t digest_out[32], uint8_t root_trace_out[32]) {
+  if (!step) return ZKL_E_INVALID;
+  return run_guarded(nullptr, [&] { step_digest(step, len, digest_out, root_trace_out); });
 }
 
 int zkl_hip_device_count(int* count) {

@@ -16,6 +16,7 @@ __all__ = [
     "F128", "ProofOptions", "AirPublicInputs", "ZklError", "Context", "load_library",
     "select_partitions_for_trace", "proof_options", "synth_vm_segment", "STAGE_NAMES",
     "FM_VM", "FM_VM_EXPECT", "FM_POSEIDON", "FM_SPONGE", "FM_MERKLE", "FM_RAM",
+    "VmArg", "StepInfo", "step_proof_encode", "step_proof_digest",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -76,6 +77,33 @@ class AirPublicInputs(C.Structure):
     ]
 
 
+class VmArg(C.Structure):
+    """zk_lisp_proof::pi::VmArg: tag 0 = U64, 1 = U128 (LE bytes), 2 = Bytes32."""
+    _fields_ = [("tag", C.c_uint32), ("bytes", C.c_uint8 * 32)]
+
+
+class StepInfo(C.Structure):
+    """zkl_step_info: what prove_segment (prove.rs:1057-1175) passes to the zl1 wrapper
+    besides the inner proof and the AirPublicInputs."""
+    _fields_ = [
+        ("suite_id", C.c_uint8 * 32),
+        ("lambda_bits", C.c_uint32),
+        ("segment_index", C.c_uint32),
+        ("segments_total", C.c_uint32),
+        ("pc_init", C.c_uint8 * 32),
+        ("state_in_hash", C.c_uint8 * 32),
+        ("state_out_hash", C.c_uint8 * 32),
+        ("ram_gp_unsorted_in", C.c_uint8 * 32),
+        ("ram_gp_unsorted_out", C.c_uint8 * 32),
+        ("ram_gp_sorted_in", C.c_uint8 * 32),
+        ("ram_gp_sorted_out", C.c_uint8 * 32),
+        ("rom_s_in", (C.c_uint8 * 32) * 3),
+        ("rom_s_out", (C.c_uint8 * 32) * 3),
+        ("n_main_args", C.c_uint32),
+        ("main_args", VmArg * 8),
+    ]
+
+
 _lib = None
 
 
@@ -113,6 +141,10 @@ def load_library():
     lib.zkl_hip_merkle_tree.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
     lib.zkl_hip_poseidon_permute.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int]
     lib.zkl_hip_set_hash_policy.argtypes = [C.c_int, C.c_uint32]
+    lib.zkl_hip_set_kernel_timing.argtypes = [C.c_void_p, C.c_int]
+    lib.zkl_step_proof_encode.argtypes = [P(AirPublicInputs), P(StepInfo), C.c_char_p, C.c_size_t,
+                                          P(P(C.c_uint8)), P(C.c_size_t)]
+    lib.zkl_step_proof_digest.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_void_p]
     lib.zkl_hip_lde.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]
     _lib = lib
     return lib
@@ -131,6 +163,29 @@ def select_partitions_for_trace(width: int, length: int):
     np_, rate = C.c_uint32(), C.c_uint32()
     lib.zkl_select_partitions(width, length, C.byref(np_), C.byref(rate))
     return np_.value, rate.value
+
+
+def step_proof_encode(pi: AirPublicInputs, info: StepInfo, inner: bytes) -> bytes:
+    """StepProof::to_bytes (proof/step.rs:79-151) of the zl1 step proof around `inner`."""
+    lib = load_library()
+    out = C.POINTER(C.c_uint8)()
+    ln = C.c_size_t()
+    rc = lib.zkl_step_proof_encode(C.byref(pi), C.byref(info), inner, len(inner), C.byref(out), C.byref(ln))
+    if rc:
+        raise ZklError(rc, lib.zkl_hip_last_error(None).decode())
+    data = C.string_at(out, ln.value)
+    lib.zkl_hip_free(out)
+    return data
+
+
+def step_proof_digest(step: bytes):
+    """(step digest, zl1 root_trace) of a ZKLSTP1 encoding (digest.rs:16-68, format.rs:214-238)."""
+    lib = load_library()
+    d, r = (C.c_uint8 * 32)(), (C.c_uint8 * 32)()
+    rc = lib.zkl_step_proof_digest(step, len(step), d, r)
+    if rc:
+        raise ZklError(rc, lib.zkl_hip_last_error(None).decode())
+    return bytes(d), bytes(r)
 
 
 def proof_options(width, length, queries=64, blowup=16, grind=16) -> ProofOptions:
@@ -256,6 +311,12 @@ class Context:
     def hash_rows(self, d_mat, n_cols, n_rows, num_partitions, hash_rate, d_out):
         rc = self.lib.zkl_hip_hash_rows(self.ptr, C.c_void_p(d_mat), n_cols, n_rows, num_partitions, hash_rate,
                                         C.c_void_p(d_out))
+        if rc:
+            self._err(rc)
+
+    def set_kernel_timing(self, mode: int):
+        """0: no kernel-family events, 1: trace row hash only (default), 2: every family."""
+        rc = self.lib.zkl_hip_set_kernel_timing(self.ptr, mode)
         if rc:
             self._err(rc)
 
