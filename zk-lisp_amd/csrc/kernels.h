@@ -103,6 +103,7 @@ struct ProofConsts {
   CeParams ce;
   fe alpha[1024];  // transition composition coefficients
   fe deep[512];   // DEEP coefficients (trace then composition columns)
+  uint32_t deep_m[512][5];  // the same as 26-bit limbs of g * 2^156 mod p (deep_kernel)
 };
 void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab,
                             const fe* d_bm /* (n_bcols + 1) x ce */, const CeParams& p, ProofConsts* dK,

@@ -26,8 +26,15 @@ void upload_air_consts(ProofConsts* dK, const AirDevice& a, hipStream_t s) {
 void upload_alphas_from_device(ProofConsts* dK, const fe* d, int n, hipStream_t s) {
   (void)hipMemcpyAsync(dK->alpha, d, sizeof(fe) * n, hipMemcpyDeviceToDevice, s);
 }
+static void limbs26(fe a, uint32_t l[5]);
 void upload_deep_coeffs(ProofConsts* dK, const fe* h, int n, hipStream_t s) {
   (void)hipMemcpyAsync(dK->deep, h, sizeof(fe) * n, hipMemcpyHostToDevice, s);
+  static thread_local std::vector<uint32_t> m;
+  m.assign((size_t)n * 5, 0);
+  const fe R = fe_pow64(fe{2, 0}, 156);
+  for (int i = 0; i < n; i++) limbs26(fe_mul(h[i], R), &m[(size_t)i * 5]);
+  (void)hipMemcpyAsync(dK->deep_m, m.data(), m.size() * 4, hipMemcpyHostToDevice, s);
+  (void)hipStreamSynchronize(s);  // m is reused by the next proof on this thread
 }
 
 // =====================================================================================
@@ -1272,25 +1279,89 @@ void launch_ood(const OodArgs& A, fe* d_partial, hipStream_t s) {
 
 // DEEP composition over the LDE domain (agg/trace.rs:1126-1218 restates the formula):
 // sum_i g_i [(T_i(x)-T_i(z))/(x-z) + (T_i(x)-T_i(zg))/(x-zg)] + same for H_j
+//   = [(S(x) - S(z)) (x - zg) + (S(x) - S(zg)) (x - z)] / ((x - z)(x - zg)),  S = sum_i g_i T_i.
+// S(x) is one lazily reduced dot product per point: the coefficients as Montgomery limbs
+// (g R, uniform -> SGPR operands), each column value split into 26-bit limbs, 25
+// v_mad_u64_u32 per column into 64-bit columns (211 terms of < 2^54 stay below 2^64) and a
+// single REDC.  Each thread takes DEEP_PTS points T apart (coalesced), keeps
+// DEEP_COLS x DEEP_PTS loads in flight, and shares one inversion among its points.
+constexpr int DEEP_PTS = 4, DEEP_COLS = 4;
+
+// canonical element of the REDC output limbs (normalised, value < 2^130)
+__device__ __forceinline__ fe limbs_canon(const uint32_t l[5]) {
+  typedef unsigned __int128 u128;
+  const u128 v = (u128)l[0] | ((u128)l[1] << 26) | ((u128)l[2] << 52) | ((u128)l[3] << 78) | ((u128)(l[4] & 0xFFFFFFu) << 104);
+  const u128 P = ((u128)P_HI << 64) | P_LO;
+  u128 r = v + (u128)(l[4] >> 24) * C_RED;  // bits >= 128: 2^128 == C_RED
+  if (r < v) r += C_RED;
+  if (r >= P) r -= P;
+  return fe{(uint64_t)r, (uint64_t)(r >> 64)};
+}
+
 __global__ __launch_bounds__(256) void deep_kernel(const fe* __restrict__ lde, const fe* __restrict__ clde,
                                                    const fe* __restrict__ roots, int shift, DeepParams p,
                                                    const ProofConsts* __restrict__ K, fe* out) {
-  const fe* c_deep = K->deep;
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p.N) return;
-  uint32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (uint32_t c = 0; c < p.W; c++) mul_acc(c_deep[c], lde[(size_t)c * p.N + i], acc);
-  for (uint32_t j = 0; j < p.C; j++) mul_acc(c_deep[p.W + j], clde[(size_t)j * p.N + i], acc);
-  fe sv = reduce288(acc);
-  fe x = fe_mul(fe{3, 0}, roots[i << shift]);
-  fe d1 = fe_sub(x, p.z), d2 = fe_sub(x, p.zg);
-  fe num = fe_add(fe_mul(fe_sub(sv, p.sz), d2), fe_mul(fe_sub(sv, p.szg), d1));
-  out[i] = fe_mul(num, fe_inv(fe_mul(d1, d2)));
+  const size_t T = (size_t)gridDim.x * blockDim.x;
+  const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t col[DEEP_PTS][10];
+#pragma unroll
+  for (int k = 0; k < DEEP_PTS; k++)
+#pragma unroll
+    for (int u = 0; u < 10; u++) col[k][u] = 0;
+  const uint32_t ncol = p.W + p.C;
+  for (uint32_t c0 = 0; c0 < ncol; c0 += DEEP_COLS) {
+    fe v[DEEP_COLS][DEEP_PTS];
+#pragma unroll
+    for (int cc = 0; cc < DEEP_COLS; cc++) {
+      const uint32_t c = c0 + cc;
+      const fe* src = c < p.W ? lde + (size_t)c * p.N : clde + (size_t)(c - p.W) * p.N;
+#pragma unroll
+      for (int k = 0; k < DEEP_PTS; k++) v[cc][k] = c < ncol ? src[i0 + k * T] : fe_zero();
+    }
+#pragma unroll
+    for (int cc = 0; cc < DEEP_COLS; cc++) {
+      const uint32_t c = min(c0 + cc, ncol - 1);  // a padded column contributes g * 0
+      const uint32_t* g = K->deep_m[c];
+      const uint32_t gm[5] = {g[0], g[1], g[2], g[3], g[4]};
+#pragma unroll
+      for (int k = 0; k < DEEP_PTS; k++) {
+        uint32_t l[5];
+        to26(v[cc][k], l);
+        mac5(l, gm, col[k]);
+      }
+    }
+  }
+  fe num[DEEP_PTS], den[DEEP_PTS];
+#pragma unroll
+  for (int k = 0; k < DEEP_PTS; k++) {
+    uint32_t l[5];
+    redc(col[k], l);
+    const fe sv = limbs_canon(l);
+    const fe x = fe_mul(fe{3, 0}, roots[(i0 + k * T) << shift]);
+    const fe d1 = fe_sub(x, p.z), d2 = fe_sub(x, p.zg);
+    num[k] = fe_add(fe_mul(fe_sub(sv, p.sz), d2), fe_mul(fe_sub(sv, p.szg), d1));
+    den[k] = fe_mul(d1, d2);
+  }
+  // batch inversion of the DEEP_PTS denominators (x is never z or zg: z is drawn outside
+  // the LDE domain, as Winterfell requires)
+  fe pre[DEEP_PTS];
+  pre[0] = den[0];
+#pragma unroll
+  for (int k = 1; k < DEEP_PTS; k++) pre[k] = fe_mul(pre[k - 1], den[k]);
+  fe inv = fe_inv(pre[DEEP_PTS - 1]);
+#pragma unroll
+  for (int k = DEEP_PTS - 1; k > 0; k--) {
+    out[i0 + k * T] = fe_mul(num[k], fe_mul(inv, pre[k - 1]));
+    inv = fe_mul(inv, den[k]);
+  }
+  out[i0] = fe_mul(num[0], inv);
 }
 void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p,
                  const ProofConsts* dK, fe* d_out, hipStream_t s) {
-  deep_kernel<<<(unsigned)((p.N + 255) / 256), 256, 0, s>>>(d_lde, d_clde, d_roots, ilog2s(Ntab) - ilog2s(p.N), p, dK,
-                                                            d_out);
+  // N is a power of two >= 64: every thread gets exactly DEEP_PTS points
+  const size_t threads = std::min<size_t>(256, p.N / DEEP_PTS);
+  deep_kernel<<<(unsigned)(p.N / (threads * DEEP_PTS)), (unsigned)threads, 0, s>>>(
+      d_lde, d_clde, d_roots, ilog2s(Ntab) - ilog2s(p.N), p, dK, d_out);
 }
 
 // FRI layer leaves: hash_elements([e_i, e_{i+Nd/2}]) (FriProver::build_layer, folding 2)
