@@ -188,6 +188,9 @@ int zkl_hip_poseidon_permute(zkl_ctx* ctx, void* d_states, uint32_t n_states, in
  * pm_min_items states (default 16384) on the matrix-core permutation, engine 0 keeps every
  * level on lane groups.  Both give identical digests; this only moves time. */
 int zkl_hip_set_hash_policy(int engine, uint32_t pm_min_items);
+/* Process-wide NTT form for evaluation (DIT) passes: 1 (default) lazily reduced 26-bit limbs
+ * inside a pass, 0 the canonical-form kernel.  Identical results; for parity tests / A-B. */
+int zkl_hip_set_ntt_mode(int lazy);
 /* Coset low-degree extension of column-major n_cols x n_rows evaluations over
  * GENERATOR * <w_{n*blowup}>; writes coefficients (n_cols x n_rows) and the LDE
  * (n_cols x n_rows*blowup), both column-major, natural order. */

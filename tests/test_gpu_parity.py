@@ -486,3 +486,30 @@ def test_step_proof_of_gpu_proof(oracle, gpu_ctx):
     want = oracle.step_encode(opi, info, oracle.prove(ot, w, n, opi, oo))
     assert step == want
     assert zkl_hip.step_proof_digest(step) == oracle.step_digest(want)
+
+
+@pytest.mark.parametrize("ncols,log_n,blow", [(64, 10, 8), (204, 9, 16), (3, 12, 2), (7, 6, 64)])
+def test_lde_lazy_ntt_matches_canonical(gpu_ctx, ncols, log_n, blow):
+    """The lazily reduced DIT passes (default) give the same LDE bytes as the canonical-form
+    kernel, on inputs biased towards p - 1 (largest limbs) and random elements."""
+    import zkl_hip
+    lib = zkl_hip.load_library()
+    rng = random.Random(ncols + log_n)
+    P = 2**128 - 45 * 2**40 + 1
+    n = 1 << log_n
+    N = n * blow
+    vals = [P - 1 - rng.randrange(2**20) if rng.random() < 0.5 else rng.randrange(P) for _ in range(ncols * n)]
+    raw = (C.c_uint8 * (16 * ncols * n)).from_buffer_copy(b"".join(v.to_bytes(16, "little") for v in vals))
+    d_v, d_c, d_l = gpu_ctx.alloc(len(raw)), gpu_ctx.alloc(len(raw)), gpu_ctx.alloc(16 * ncols * N)
+    gpu_ctx.upload(d_v, raw, len(raw))
+    outs = []
+    try:
+        for lazy in (0, 1):
+            assert lib.zkl_hip_set_ntt_mode(lazy) == 0
+            gpu_ctx.lde(d_v, ncols, n, blow, d_c, d_l)
+            outs.append(gpu_ctx.download(d_l, 16 * ncols * N))
+    finally:
+        lib.zkl_hip_set_ntt_mode(1)
+        for d in (d_v, d_c, d_l):
+            gpu_ctx.free(d)
+    assert outs[0] == outs[1]

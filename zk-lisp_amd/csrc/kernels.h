@@ -30,6 +30,8 @@ void upload_pm_tables(const HasherConsts& h, hipStream_t s);
 // 1 = matrix-core permutation on throughput-bound levels (default), 0 = lane groups only
 int hash_engine();
 void set_hash_policy(int engine, size_t min_items);
+// DIT passes on lazily reduced limbs (default) or the canonical kernel
+void set_ntt_lazy(bool on);
 // n Poseidon permutations of 12-element canonical states in place (engine as above)
 void launch_permute(fe* d_states, size_t n, int engine, hipStream_t s);
 struct CeParams;

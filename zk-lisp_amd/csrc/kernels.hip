@@ -780,6 +780,142 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_pass_kernel(fe* __restrict__ 
   }
 }
 
+// DIT pass with lazily reduced 26-bit limbs (the LDE evaluation passes).  Elements enter
+// LDS as five limbs (struct of arrays), every butterfly is v = REDC(x1 * wR) (normalised,
+// < 2^130), y0 = x0 + v, y1 = x0 + Q - v with Q = 8p written with every limb >= 2^26, and
+// only the pass output is reduced to canonical form.  Limbs grow by at most 2^27 per stage,
+// so after 8 stages they stay below 2^31 and every product term stays below 2^57 (the
+// REDC input bound).  ~40% fewer instructions per butterfly than the canonical form
+// (no per-butterfly canonicalisation, limbwise add/sub).
+constexpr uint32_t NTT_Q[5] = {67108872u, 128319487u, 134217726u, 134217726u, 134217726u};  // 8p
+
+__device__ __forceinline__ fe ntt_canon(const uint32_t l[5]) {
+  typedef unsigned __int128 u128;
+  // limbs < 2^31: the low part is < 2^110, adding limb 4's low 24 bits at 2^104 may carry
+  // past 2^128, and limb 4's high bits sit at 2^128 (t < 2^7)
+  const u128 lo = (u128)l[0] + ((u128)l[1] << 26) + ((u128)l[2] << 52) + ((u128)l[3] << 78);
+  const u128 v = lo + ((u128)(l[4] & 0xFFFFFFu) << 104);
+  const uint32_t t = (l[4] >> 24) + (v < lo ? 1u : 0u);
+  const u128 P = ((u128)P_HI << 64) | P_LO;
+  u128 r = v + (u128)t * C_RED;  // 2^128 == C_RED
+  if (r < v) r += C_RED;
+  if (r >= P) r -= P;
+  return fe{(uint64_t)r, (uint64_t)(r >> 64)};
+}
+
+__global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restrict__ data, size_t ncols, int logN, int r,
+                                                                  int logS, MontTab roots, const fe* __restrict__ src,
+                                                                  int src_logb) {
+  constexpr int PITCHED = NTT_ELEMS + NTT_ELEMS / 16;
+  __shared__ uint32_t buf[5][PITCHED];
+  const int R = 1 << r;
+  const int G = NTT_ELEMS >> r;
+  const size_t S = (size_t)1 << logS;
+  const int log_gpc = logN - r;
+  const size_t gpc = (size_t)1 << log_gpc;
+  const bool gfast = S >= (size_t)G;
+  const int pitch = R >= 16 ? R + 1 : R;
+  size_t col_fixed = 0, qbase = 0;
+  const bool whole = gpc >= (size_t)G;
+  if (whole) {
+    col_fixed = blockIdx.x % (unsigned)ncols;
+    qbase = (size_t)(blockIdx.x / (unsigned)ncols) * G;
+  }
+  auto locate = [&](int g, size_t& col, size_t& q) -> bool {
+    if (whole) {
+      col = col_fixed;
+      q = qbase + g;
+      return true;
+    }
+    const size_t qg = (size_t)blockIdx.x * G + g;
+    col = qg >> log_gpc;
+    q = qg & (gpc - 1);
+    return col < ncols;
+  };
+  auto addr = [&](int g, int t, bool& ok) -> size_t {
+    size_t col, q;
+    ok = locate(g, col, q);
+    const size_t L = q & (S - 1), Hb = q >> logS;
+    return (col << logN) + ((Hb << logS) << r) + (size_t)t * S + L;
+  };
+  const size_t Nmask = ((size_t)1 << logN) - 1;
+  for (int e = threadIdx.x; e < NTT_ELEMS; e += NTT_THREADS) {
+    const int g = gfast ? (e % G) : (e >> r);
+    const int t = gfast ? (e / G) : (e & (R - 1));
+    bool ok;
+    const size_t a = addr(g, t, ok);
+    fe v = fe_zero();
+    if (ok) v = src ? src[((a >> logN) << (logN - src_logb)) + ((a & Nmask) >> src_logb)] : data[a];
+    uint32_t l[5];
+    to26(v, l);
+#pragma unroll
+    for (int i = 0; i < 5; i++) buf[i][g * pitch + t] = l[i];
+  }
+  __syncthreads();
+  for (int lh = 0; lh < r; lh++) {
+    const int h = 1 << lh;
+    const size_t Hs = (size_t)h << logS;
+    constexpr int BPT = NTT_ELEMS / 2 / NTT_THREADS;
+    uint32_t x0[BPT][5], x1[BPT][5];
+    size_t te[BPT];
+    int o0[BPT];
+#pragma unroll
+    for (int i = 0; i < BPT; i++) {
+      const int u = threadIdx.x + NTT_THREADS * i;
+      const int g = u % G;
+      const int w = u / G;
+      const int k = w & (h - 1);
+      const int t0 = ((w >> lh) << (lh + 1)) + k;
+      size_t colx, q;
+      locate(g, colx, q);
+      te[i] = Hs + ((size_t)k << logS) + (q & (S - 1));
+      o0[i] = g * pitch + t0;
+#pragma unroll
+      for (int l = 0; l < 5; l++) {
+        x0[i][l] = buf[l][o0[i]];
+        x1[i][l] = buf[l][o0[i] + h];
+      }
+    }
+    // a thread's butterflies touch only their own positions: no barrier between load and store
+#pragma unroll
+    for (int i = 0; i < BPT; i++) {
+      const uint4 q4 = roots.l4[te[i]];
+      const uint32_t wm[5] = {q4.x, q4.y, q4.z, q4.w, roots.l1[te[i]]};
+      uint32_t v[5];
+      mont_mul(x1[i], wm, v);
+#pragma unroll
+      for (int l = 0; l < 5; l++) {
+        buf[l][o0[i]] = x0[i][l] + v[l];
+        buf[l][o0[i] + h] = x0[i][l] + NTT_Q[l] - v[l];
+      }
+    }
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < NTT_ELEMS; e += NTT_THREADS) {
+    const int g = gfast ? (e % G) : (e >> r);
+    const int t = gfast ? (e / G) : (e & (R - 1));
+    bool ok;
+    const size_t a = addr(g, t, ok);
+    uint32_t l[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) l[i] = buf[i][g * pitch + t];
+    if (ok) data[a] = ntt_canon(l);
+  }
+}
+
+// DIT form: lazy limbs (default) or the canonical kernel (ZKL_NTT=classic, set_ntt_lazy)
+static std::atomic<int> g_ntt_lazy{-1};
+static bool ntt_lazy_enabled() {
+  int v = g_ntt_lazy.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("ZKL_NTT");
+    v = (e && !strcmp(e, "classic")) ? 0 : 1;
+    g_ntt_lazy.store(v);
+  }
+  return v != 0;
+}
+void set_ntt_lazy(bool on) { g_ntt_lazy.store(on ? 1 : 0); }
+
 static int ilog2s(size_t n) { int k = 0; while (((size_t)1 << k) < n) k++; return k; }
 
 static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, MontTab roots, size_t Ntab,
@@ -803,8 +939,12 @@ static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
       int r = std::min(8, hi - cur + 1);
       size_t groups = (N >> r) * ncols;
       size_t G = NTT_ELEMS >> r;
-      ntt_pass_kernel<false><<<(unsigned)((groups + G - 1) / G), NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots, logTab,
-                                                                              cur == lo ? src : nullptr, src_logb);
+      if (ntt_lazy_enabled())
+        ntt_dit_lazy_kernel<<<(unsigned)((groups + G - 1) / G), NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots,
+                                                                                    cur == lo ? src : nullptr, src_logb);
+      else
+        ntt_pass_kernel<false><<<(unsigned)((groups + G - 1) / G), NTT_THREADS, 0, s>>>(
+            d, ncols, logN, r, cur, roots, logTab, cur == lo ? src : nullptr, src_logb);
       cur += r;
     }
   }

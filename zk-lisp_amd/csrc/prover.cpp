@@ -933,6 +933,12 @@ int zkl_hip_hash_rows(zkl_ctx* c, const void* d_m, uint32_t nc, uint32_t nr, uin
   });
 }
 
+int zkl_hip_set_ntt_mode(int lazy) {
+  if (lazy < 0 || lazy > 1) return ZKL_E_INVALID;
+  set_ntt_lazy(lazy != 0);
+  return 0;
+}
+
 int zkl_hip_set_hash_policy(int engine, uint32_t pm_min_items) {
   if (engine < 0 || engine > 1) return ZKL_E_INVALID;
   set_hash_policy(engine, pm_min_items);

@@ -141,6 +141,7 @@ def load_library():
     lib.zkl_hip_merkle_tree.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
     lib.zkl_hip_poseidon_permute.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int]
     lib.zkl_hip_set_hash_policy.argtypes = [C.c_int, C.c_uint32]
+    lib.zkl_hip_set_ntt_mode.argtypes = [C.c_int]
     lib.zkl_hip_set_kernel_timing.argtypes = [C.c_void_p, C.c_int]
     lib.zkl_step_proof_encode.argtypes = [P(AirPublicInputs), P(StepInfo), C.c_char_p, C.c_size_t,
                                           P(P(C.c_uint8)), P(C.c_size_t)]
