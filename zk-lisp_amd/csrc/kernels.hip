@@ -807,7 +807,8 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
                                                                   int logS, MontTab roots, const fe* __restrict__ src,
                                                                   int src_logb) {
   constexpr int PITCHED = NTT_ELEMS + NTT_ELEMS / 16;
-  __shared__ uint32_t buf[5][PITCHED];
+  __shared__ uint4 bufA[PITCHED];     // limbs 0..3 (16-byte accesses, as the canonical kernel)
+  __shared__ uint32_t bufB[PITCHED];  // limb 4
   const int R = 1 << r;
   const int G = NTT_ELEMS >> r;
   const size_t S = (size_t)1 << logS;
@@ -848,8 +849,8 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
     if (ok) v = src ? src[((a >> logN) << (logN - src_logb)) + ((a & Nmask) >> src_logb)] : data[a];
     uint32_t l[5];
     to26(v, l);
-#pragma unroll
-    for (int i = 0; i < 5; i++) buf[i][g * pitch + t] = l[i];
+    bufA[g * pitch + t] = make_uint4(l[0], l[1], l[2], l[3]);
+    bufB[g * pitch + t] = l[4];
   }
   __syncthreads();
   for (int lh = 0; lh < r; lh++) {
@@ -870,11 +871,9 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
       locate(g, colx, q);
       te[i] = Hs + ((size_t)k << logS) + (q & (S - 1));
       o0[i] = g * pitch + t0;
-#pragma unroll
-      for (int l = 0; l < 5; l++) {
-        x0[i][l] = buf[l][o0[i]];
-        x1[i][l] = buf[l][o0[i] + h];
-      }
+      const uint4 a0 = bufA[o0[i]], a1 = bufA[o0[i] + h];
+      x0[i][0] = a0.x; x0[i][1] = a0.y; x0[i][2] = a0.z; x0[i][3] = a0.w; x0[i][4] = bufB[o0[i]];
+      x1[i][0] = a1.x; x1[i][1] = a1.y; x1[i][2] = a1.z; x1[i][3] = a1.w; x1[i][4] = bufB[o0[i] + h];
     }
     // a thread's butterflies touch only their own positions: no barrier between load and store
 #pragma unroll
@@ -883,11 +882,16 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
       const uint32_t wm[5] = {q4.x, q4.y, q4.z, q4.w, roots.l1[te[i]]};
       uint32_t v[5];
       mont_mul(x1[i], wm, v);
+      uint32_t y0[5], y1[5];
 #pragma unroll
       for (int l = 0; l < 5; l++) {
-        buf[l][o0[i]] = x0[i][l] + v[l];
-        buf[l][o0[i] + h] = x0[i][l] + NTT_Q[l] - v[l];
+        y0[l] = x0[i][l] + v[l];
+        y1[l] = x0[i][l] + NTT_Q[l] - v[l];
       }
+      bufA[o0[i]] = make_uint4(y0[0], y0[1], y0[2], y0[3]);
+      bufB[o0[i]] = y0[4];
+      bufA[o0[i] + h] = make_uint4(y1[0], y1[1], y1[2], y1[3]);
+      bufB[o0[i] + h] = y1[4];
     }
     __syncthreads();
   }
@@ -896,9 +900,8 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
     const int t = gfast ? (e / G) : (e & (R - 1));
     bool ok;
     const size_t a = addr(g, t, ok);
-    uint32_t l[5];
-#pragma unroll
-    for (int i = 0; i < 5; i++) l[i] = buf[i][g * pitch + t];
+    const uint4 a4 = bufA[g * pitch + t];
+    const uint32_t l[5] = {a4.x, a4.y, a4.z, a4.w, bufB[g * pitch + t]};
     if (ok) data[a] = ntt_canon(l);
   }
 }
