@@ -853,13 +853,61 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
     bufB[g * pitch + t] = l[4];
   }
   __syncthreads();
-  for (int lh = 0; lh < r; lh++) {
+  auto ld = [&](int o, uint32_t x[5]) {
+    const uint4 a = bufA[o];
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = bufB[o];
+  };
+  auto st = [&](int o, const uint32_t x[5]) {
+    bufA[o] = make_uint4(x[0], x[1], x[2], x[3]);
+    bufB[o] = x[4];
+  };
+  auto tw = [&](size_t e, uint32_t wm[5]) {
+    const uint4 q4 = roots.l4[e];
+    wm[0] = q4.x; wm[1] = q4.y; wm[2] = q4.z; wm[3] = q4.w; wm[4] = roots.l1[e];
+  };
+  // y0 = x0 + x1 w, y1 = x0 - x1 w (+Q), in place
+  auto bfly = [&](uint32_t x0[5], uint32_t x1[5], const uint32_t wm[5]) {
+    uint32_t v[5];
+    mont_mul(x1, wm, v);
+#pragma unroll
+    for (int l = 0; l < 5; l++) {
+      x1[l] = x0[l] + NTT_Q[l] - v[l];
+      x0[l] = x0[l] + v[l];
+    }
+  };
+  int lh = 0;
+  // two stages per LDS round trip: a thread takes the quad t0, t0+h, t0+2h, t0+3h of one
+  // group; stage lh pairs (0,1), (2,3) under one twiddle, stage lh+1 pairs (0,2), (1,3)
+  for (; lh + 1 < r; lh += 2) {
     const int h = 1 << lh;
-    const size_t Hs = (size_t)h << logS;
+    constexpr int QPT = NTT_ELEMS / 4 / NTT_THREADS;
+#pragma unroll
+    for (int i = 0; i < QPT; i++) {
+      const int u = threadIdx.x + NTT_THREADS * i;
+      const int g = u % G;
+      const int w = u / G;
+      const int k = w & (h - 1);
+      const int t0 = ((w >> lh) << (lh + 2)) + k;
+      size_t colx, q;
+      locate(g, colx, q);
+      const size_t L = q & (S - 1);
+      const int o = g * pitch + t0;
+      uint32_t a0[5], a1[5], a2[5], a3[5], w1[5], w2[5], w3[5];
+      ld(o, a0); ld(o + h, a1); ld(o + 2 * h, a2); ld(o + 3 * h, a3);
+      tw(((size_t)h << logS) + ((size_t)k << logS) + L, w1);
+      tw(((size_t)(2 * h) << logS) + ((size_t)k << logS) + L, w2);
+      tw(((size_t)(2 * h) << logS) + ((size_t)(k + h) << logS) + L, w3);
+      bfly(a0, a1, w1);
+      bfly(a2, a3, w1);
+      bfly(a0, a2, w2);
+      bfly(a1, a3, w3);
+      st(o, a0); st(o + h, a1); st(o + 2 * h, a2); st(o + 3 * h, a3);
+    }
+    __syncthreads();
+  }
+  if (lh < r) {  // odd stage count: one radix-2 stage
+    const int h = 1 << lh;
     constexpr int BPT = NTT_ELEMS / 2 / NTT_THREADS;
-    uint32_t x0[BPT][5], x1[BPT][5];
-    size_t te[BPT];
-    int o0[BPT];
 #pragma unroll
     for (int i = 0; i < BPT; i++) {
       const int u = threadIdx.x + NTT_THREADS * i;
@@ -869,29 +917,12 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
       const int t0 = ((w >> lh) << (lh + 1)) + k;
       size_t colx, q;
       locate(g, colx, q);
-      te[i] = Hs + ((size_t)k << logS) + (q & (S - 1));
-      o0[i] = g * pitch + t0;
-      const uint4 a0 = bufA[o0[i]], a1 = bufA[o0[i] + h];
-      x0[i][0] = a0.x; x0[i][1] = a0.y; x0[i][2] = a0.z; x0[i][3] = a0.w; x0[i][4] = bufB[o0[i]];
-      x1[i][0] = a1.x; x1[i][1] = a1.y; x1[i][2] = a1.z; x1[i][3] = a1.w; x1[i][4] = bufB[o0[i] + h];
-    }
-    // a thread's butterflies touch only their own positions: no barrier between load and store
-#pragma unroll
-    for (int i = 0; i < BPT; i++) {
-      const uint4 q4 = roots.l4[te[i]];
-      const uint32_t wm[5] = {q4.x, q4.y, q4.z, q4.w, roots.l1[te[i]]};
-      uint32_t v[5];
-      mont_mul(x1[i], wm, v);
-      uint32_t y0[5], y1[5];
-#pragma unroll
-      for (int l = 0; l < 5; l++) {
-        y0[l] = x0[i][l] + v[l];
-        y1[l] = x0[i][l] + NTT_Q[l] - v[l];
-      }
-      bufA[o0[i]] = make_uint4(y0[0], y0[1], y0[2], y0[3]);
-      bufB[o0[i]] = y0[4];
-      bufA[o0[i] + h] = make_uint4(y1[0], y1[1], y1[2], y1[3]);
-      bufB[o0[i] + h] = y1[4];
+      const int o = g * pitch + t0;
+      uint32_t x0[5], x1[5], wm[5];
+      ld(o, x0); ld(o + h, x1);
+      tw(((size_t)h << logS) + ((size_t)k << logS) + (q & (S - 1)), wm);
+      bfly(x0, x1, wm);
+      st(o, x0); st(o + h, x1);
     }
     __syncthreads();
   }
