@@ -217,6 +217,23 @@ def main():
         ctx.prove_segment_device(d_trace, W, n, pi, opts)
         fam = ctx.kernel_times()
         ctx.set_kernel_timing(1)
+    # Aggregation hand-off (untimed): every rank wraps its last proof as zl1
+    # step `rank` of `world` (ZKLSTP1); rank 0 gathers, orders and chain-checks them and forms
+    # the children root the aggregation proof commits to (agg/child.rs:853-895).
+    t_h = time.perf_counter()
+    info = zkl_hip.StepInfo()
+    info.suite_id[:] = bytes(pi.program_id)
+    info.lambda_bits, info.segment_index, info.segments_total = 128, rank, world
+    info.state_in_hash[:] = rank.to_bytes(32, "little")  # synthetic chain: out(r) = in(r+1)
+    info.state_out_hash[:] = (rank + 1).to_bytes(32, "little")
+    steps = dist.collect_step_proofs([zkl_hip.step_proof_encode(pi, info, proof)])
+    handoff = None
+    if steps is not None:
+        root = zkl_hip.children_root(bytes(pi.program_id), [d["digest"] for d in steps],
+                                     [d["root_trace"] for d in steps])
+        handoff = {"segments": len(steps), "step_bytes": sum(d["bytes"] for d in steps),
+                   "ms": round((time.perf_counter() - t_h) * 1e3, 2), "children_root": root[:16].hex(),
+                   "transport": "gloo (host bytes; the proofs already live in host memory)"}
 
     if rank == 0:
         value = world * args.steps / elapsed
@@ -284,6 +301,7 @@ def main():
             "kernel_ms_per_family_untimed_step": {k: round(v[0], 3) for k, v in fam.items()},
             "stage_ms_last_step": {k: round(v, 3) for k, v in stages.items()},
             "host_ms_last_step": {k: round(v, 3) for k, v in host.items()},
+            "step_handoff": handoff,
         }
         if world == 1 and args.c3_segments > 0:
             c3 = {}

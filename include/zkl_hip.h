@@ -239,6 +239,12 @@ int zkl_step_proof_encode(const zkl_air_public_inputs* pi, const zkl_step_info* 
  * (proof/digest.rs:16-68).  Either output may be NULL.  Errors: ZKL_E_INVALID with
  * zkl_hip_last_error(NULL) naming the truncated/invalid field, as step.rs does. */
 int zkl_step_proof_digest(const uint8_t* step, size_t len, uint8_t digest_out[32], uint8_t root_trace_out[32]);
+/* agg::child::children_root_from_compact (agg/child.rs:853-895): the aggregation's root
+ * over n children given as n x 32-byte step digests and n x 32-byte zl1 root_trace values
+ * (what zkl_step_proof_digest returns), under the Poseidon suite of suite_id.  Rank 0 of
+ * a multi-GPU run computes it after gathering the step proofs. */
+int zkl_children_root(const uint8_t suite_id[32], const uint8_t* digests, const uint8_t* root_traces, uint32_t n,
+                      uint8_t root_out[32]);
 
 #ifdef __cplusplus
 }

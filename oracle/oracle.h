@@ -131,5 +131,7 @@ void orc_free(void *p);
 int orc_step_encode(const zkl_air_public_inputs *pi, const zkl_step_info *s, const uint8_t *inner, size_t inner_len,
                     uint8_t **out, size_t *out_len);
 int orc_step_digest(const uint8_t *p, size_t n, uint8_t digest[32], uint8_t rt[32], char *err, size_t errlen);
+int orc_children_root(const uint8_t suite[32], const uint8_t *digests, const uint8_t *roots, uint32_t n,
+                      uint8_t out[32]);
 
 #endif

@@ -145,6 +145,35 @@ static fe ro1(const char *dom, const uint8_t *p, size_t n) {
   return ro_from_slices(dom, parts, lens, 1);
 }
 
+/* agg::child::children_root_from_compact (agg/child.rs:853-895) */
+static int cmp32(const void *a, const void *b) { return memcmp(a, b, 32); }
+
+int orc_children_root(const uint8_t suite[32], const uint8_t *digests, const uint8_t *roots, uint32_t n,
+                      uint8_t out[32]) {
+  memset(out, 0, 32);
+  if (n == 0) return 0;
+  pos_suite S;
+  pos_suite_derive(suite, POS_ROUNDS, &S);
+  uint8_t *items = (uint8_t *)calloc(n, 32);
+  fe *layer = (fe *)malloc(sizeof(fe) * n);
+  for (uint32_t i = 0; i < n; i++) {
+    fe leaf = two_lanes(&S, fold_bytes32(digests + 32 * i), fold_bytes32(roots + 32 * i));
+    fe_to_bytes(leaf, items + 32 * i); /* fe_to_bytes_fold: 16 LE bytes + 16 zero */
+  }
+  qsort(items, n, 32, cmp32);
+  size_t m = n;
+  for (size_t i = 0; i < m; i++) layer[i] = fold_bytes32(items + 32 * i);
+  while (m > 1) {
+    size_t k = 0;
+    for (size_t i = 0; i < m; i += 2) layer[k++] = two_lanes(&S, layer[i], i + 1 < m ? layer[i + 1] : layer[i]);
+    m = k;
+  }
+  fe_to_bytes(layer[0], out);
+  free(items);
+  free(layer);
+  return 0;
+}
+
 /* error text follows step.rs ("step proof truncated before <field>") */
 #define NEED(k, what)                                                        \
   do {                                                                       \

@@ -245,6 +245,13 @@ def step_encode(pi, info, inner: bytes) -> bytes:
     return data
 
 
+def children_root(suite: bytes, digests, roots) -> bytes:
+    """oracle/step.c: agg::child::children_root_from_compact restatement."""
+    out = (C.c_uint8 * 32)()
+    lib().orc_children_root(bytes(suite), b"".join(digests), b"".join(roots), C.c_uint32(len(digests)), out)
+    return bytes(out)
+
+
 def step_digest(step: bytes):
     """oracle/step.c: (digest, root_trace) or raises ValueError(message)."""
     d, r = (C.c_uint8 * 32)(), (C.c_uint8 * 32)()

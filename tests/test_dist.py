@@ -38,6 +38,97 @@ def _worker(rank, world, port, q):
     dist.shutdown()
 
 
+def _step_worker(rank, world, port, q):
+    """Rank r wraps an oracle proof of its own segment as step r of `world` (host-only
+    library calls) and hands it to rank 0, as bench.py does after the timed region."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    for p in (os.path.join(ROOT, "zk-lisp_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import ctypes as C
+    import oracle_lib
+    import zkl_hip
+    from zkl_hip import dist
+    dist.init()
+    t, opi, w = oracle_lib.synth_segment(0x5EED7000 + rank, 5)
+    inner = oracle_lib.prove(t, w, 32, opi, oracle_lib.default_options(w, 32, queries=4, grind=0))
+    pi = zkl_hip.AirPublicInputs()
+    C.memmove(C.byref(pi), C.byref(opi), C.sizeof(pi))
+    info = zkl_hip.StepInfo()
+    info.suite_id[:] = bytes(pi.program_id)
+    info.lambda_bits, info.segment_index, info.segments_total = 64, rank, world
+    info.state_in_hash[:] = bytes([rank]) * 32       # chained: out(r) = in(r+1)
+    info.state_out_hash[:] = bytes([rank + 1]) * 32
+    step = zkl_hip.step_proof_encode(pi, info, inner)
+    steps = dist.collect_step_proofs([step])
+    root = None
+    if steps is not None:
+        root = zkl_hip.children_root(bytes(pi.program_id), [d["digest"] for d in steps],
+                                     [d["root_trace"] for d in steps])
+    q.put((rank, None if steps is None else [(d["segment_index"], d["digest"], d["root_trace"]) for d in steps],
+           zkl_hip.step_proof_digest(step), root, bytes(pi.program_id)))
+    dist.shutdown()
+
+
+def test_gloo_step_handoff_world_size_2():
+    """World size 2: each rank's step proof reaches rank 0 intact (digest, root_trace),
+    ordered by segment, chain-checked, and rank 0 forms the children root over them."""
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "zk-lisp_amd"))
+    import zkl_hip
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_step_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, steps, own, root, suite = q.get(timeout=180)
+        res[r] = (steps, own, root, suite)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    steps, _, root, suite = res[0]
+    assert res[1][0] is None and res[1][2] is None
+    assert [s[0] for s in steps] == [0, 1]
+    assert (steps[0][1], steps[0][2]) == res[0][1] and (steps[1][1], steps[1][2]) == res[1][1]
+    assert root == zkl_hip.children_root(suite, [s[1] for s in steps], [s[2] for s in steps])
+    assert root != bytes(32)
+
+
+def test_step_chain_check_rejects_broken_chain():
+    """collect_step_proofs (single process: the gather is the identity) rejects a state
+    hash that does not continue the previous segment and a missing segment."""
+    sys.path.insert(0, os.path.join(ROOT, "zk-lisp_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes as C
+    import oracle_lib
+    import zkl_hip
+    from zkl_hip import dist
+    t, opi, w = oracle_lib.synth_segment(0x5EED7100, 5)
+    inner = oracle_lib.prove(t, w, 32, opi, oracle_lib.default_options(w, 32, queries=4, grind=0))
+    pi = zkl_hip.AirPublicInputs()
+    C.memmove(C.byref(pi), C.byref(opi), C.sizeof(pi))
+
+    def step(i, total, sin, sout):
+        info = zkl_hip.StepInfo()
+        info.suite_id[:] = bytes(pi.program_id)
+        info.segment_index, info.segments_total = i, total
+        info.state_in_hash[:] = bytes([sin]) * 32
+        info.state_out_hash[:] = bytes([sout]) * 32
+        return zkl_hip.step_proof_encode(pi, info, inner)
+
+    ok = dist.collect_step_proofs([step(1, 3, 1, 2), step(0, 3, 0, 1), step(2, 3, 2, 3)])
+    assert [d["segment_index"] for d in ok] == [0, 1, 2]
+    with pytest.raises(ValueError, match="state_in_hash"):
+        dist.collect_step_proofs([step(0, 2, 0, 1), step(1, 2, 5, 6)])
+    with pytest.raises(ValueError, match="exactly once"):
+        dist.collect_step_proofs([step(0, 3, 0, 1), step(2, 3, 1, 2)])
+
+
 def test_gloo_world_size_2():
     import torch.multiprocessing as mp
     with socket.socket() as s:

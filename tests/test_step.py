@@ -150,6 +150,66 @@ def test_single_segment_rule(inner):
     assert zkl_hip.step_proof_digest(a) == zkl_hip.step_proof_digest(b)
 
 
+def test_reference_step_serialization_cases(oracle, inner):
+    """The reference's own codec tests (zk-lisp-proof-winterfell/tests/step_serialization.rs):
+    a to_bytes/from_bytes round trip keeps digest, state hashes, suite, meta and core pi
+    (:48-106); a corrupted magic is rejected with a message naming it (:109-128); a buffer
+    cut to 8 bytes (:131-149) or one byte short of its inner proof (:152-170) is rejected."""
+    import zkl_hip
+    inner_b, pi = inner
+    info = _info(zkl_hip, pi, 11, ((0, 5), (2, None)), 0, 1)
+    step = zkl_hip.step_proof_encode(pi, info, inner_b)
+    d = zkl_hip.parse_step_proof(step)
+    assert d["state_in_hash"] == bytes(info.state_in_hash) and d["state_out_hash"] == bytes(info.state_out_hash)
+    assert d["suite_id"] == bytes(info.suite_id) and d["program_id"] == bytes(pi.program_id)
+    assert d["main_args"][0] == (0, (5).to_bytes(8, "little")) and d["main_args"][1][0] == 2
+    assert d["inner"] == inner_b
+    assert zkl_hip.step_proof_digest(step) == _py_digest(step)
+    bad = bytearray(step)
+    bad[0] ^= 0xFF
+    with pytest.raises(zkl_hip.ZklError, match="magic"):
+        zkl_hip.step_proof_digest(bytes(bad))
+    with pytest.raises(ValueError, match="magic"):
+        zkl_hip.parse_step_proof(bytes(bad))
+    for cut in (step[:8], step[:-1]):
+        with pytest.raises(zkl_hip.ZklError, match="truncated"):
+            zkl_hip.step_proof_digest(cut)
+        with pytest.raises(ValueError, match="truncated"):
+            oracle.step_digest(cut)
+        with pytest.raises(ValueError, match="truncated"):
+            zkl_hip.parse_step_proof(cut)
+
+
+def _py_children_root(suite, digests, roots):
+    """agg/child.rs:853-895 over pyref."""
+    if not digests:
+        return bytes(32)
+    S = pyref.suite(suite)
+
+    def two(l, r):
+        return pyref.permute([l, r] + [0] * 8 + list(S[0]), S)[0]
+
+    items = sorted(two(pyref.fold32(d), pyref.fold32(r)).to_bytes(16, "little") + bytes(16)
+                   for d, r in zip(digests, roots))
+    layer = [pyref.fold32(b) for b in items]
+    while len(layer) > 1:
+        layer = [two(layer[i], layer[i + 1] if i + 1 < len(layer) else layer[i]) for i in range(0, len(layer), 2)]
+    return layer[0].to_bytes(16, "little") + bytes(16)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 5])
+def test_children_root_three_ways(oracle, n):
+    import zkl_hip
+    rng = random.Random(100 + n)
+    suite = rng.randbytes(32)
+    digests = [rng.randbytes(16) + bytes(16) for _ in range(n)]
+    roots = [rng.randbytes(32) for _ in range(n)]
+    got = zkl_hip.children_root(suite, digests, roots)
+    assert got == oracle.children_root(suite, digests, roots) == _py_children_root(suite, digests, roots)
+    if n >= 2:  # sorted leaves: the order of the children does not matter
+        assert zkl_hip.children_root(suite, digests[::-1], roots[::-1]) == got
+
+
 def test_step_decode_errors(oracle, inner):
     """Truncations and a bad magic / VmArg tag fail in both implementations with the
     reference's messages (step.rs:158-180, 305-309)."""

@@ -28,6 +28,7 @@ namespace zkl {  // step.cpp
 std::vector<uint8_t> step_encode(const zkl_air_public_inputs& pi, const zkl_step_info& s, const uint8_t* inner,
                                  size_t inner_len);
 void step_digest(const uint8_t* p, size_t n, uint8_t digest[32], uint8_t rt[32]);
+void children_root(const uint8_t suite[32], const uint8_t* digests, const uint8_t* roots, size_t n, uint8_t out[32]);
 }  // namespace zkl
 
 namespace {
@@ -866,6 +867,12 @@ int zkl_step_proof_encode(const zkl_air_public_inputs* pi, const zkl_step_info* 
   int rc = run_guarded(nullptr, [&] { v = step_encode(*pi, *info, inner, inner_len); });
   if (rc) return rc;
   return finish_proof(v, out, out_len);
+}
+
+int zkl_children_root(const uint8_t suite_id[32], const uint8_t* digests, const uint8_t* root_traces, uint32_t n,
+                      uint8_t root_out[32]) {
+  if (!suite_id || !root_out || (n && (!digests || !root_traces))) return ZKL_E_INVALID;
+  return run_guarded(nullptr, [&] { children_root(suite_id, digests, root_traces, n, root_out); });
 }
 
 int zkl_step_proof_digest(const uint8_t* step, size_t len, uint8_t digest_out[32], uint8_t root_trace_out[32]) {

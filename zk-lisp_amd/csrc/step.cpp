@@ -3,6 +3,7 @@
 // (step.rs:153-493), the zl1 commitment echo root_trace (proof/format.rs:214-238) and the
 // step digest (proof/digest.rs:16-68).  Host-only byte work; the inner proof is the
 // Proof::to_bytes image written by prover.cpp.
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -229,6 +230,34 @@ void step_digest(const uint8_t* p, size_t n, uint8_t digest[32], uint8_t rt[32])
   Out d;
   d.fe_fold(ch);
   for (int i = 0; i < 32; i++) digest[i] = d.v[i];
+}
+
+// agg::child::children_root_from_compact (agg/child.rs:853-895): leaf_i =
+// two_lanes(fold(step_digest_i), fold(root_trace_i)) as 32 folded bytes, leaves sorted
+// bytewise, then pairwise two_lanes levels (an odd tail pairs with itself); [0; 32] when empty.
+void children_root(const uint8_t suite[32], const uint8_t* digests, const uint8_t* roots, size_t n, uint8_t out[32]) {
+  for (int i = 0; i < 32; i++) out[i] = 0;
+  if (n == 0) return;
+  const PoseidonSuite S = derive_poseidon_suite(suite, 27);
+  std::vector<std::vector<uint8_t>> items(n);
+  for (size_t i = 0; i < n; i++) {
+    const fe leaf = two_lanes(S, fold_bytes32(digests + 32 * i), fold_bytes32(roots + 32 * i));
+    Out o;
+    o.fe_fold(leaf);
+    items[i] = o.v;
+  }
+  std::sort(items.begin(), items.end());  // lexicographic, as [u8; 32]::sort_unstable
+  std::vector<fe> layer;
+  for (auto& it : items) layer.push_back(fold_bytes32(it.data()));
+  while (layer.size() > 1) {
+    std::vector<fe> next;
+    for (size_t i = 0; i < layer.size(); i += 2)
+      next.push_back(two_lanes(S, layer[i], i + 1 < layer.size() ? layer[i + 1] : layer[i]));
+    layer.swap(next);
+  }
+  Out o;
+  o.fe_fold(layer[0]);
+  for (int i = 0; i < 32; i++) out[i] = o.v[i];
 }
 
 }  // namespace zkl

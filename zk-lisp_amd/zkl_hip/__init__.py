@@ -16,7 +16,7 @@ __all__ = [
     "F128", "ProofOptions", "AirPublicInputs", "ZklError", "Context", "load_library",
     "select_partitions_for_trace", "proof_options", "synth_vm_segment", "STAGE_NAMES",
     "FM_VM", "FM_VM_EXPECT", "FM_POSEIDON", "FM_SPONGE", "FM_MERKLE", "FM_RAM",
-    "VmArg", "StepInfo", "step_proof_encode", "step_proof_digest",
+    "VmArg", "StepInfo", "step_proof_encode", "step_proof_digest", "parse_step_proof", "children_root",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -146,6 +146,7 @@ def load_library():
     lib.zkl_step_proof_encode.argtypes = [P(AirPublicInputs), P(StepInfo), C.c_char_p, C.c_size_t,
                                           P(P(C.c_uint8)), P(C.c_size_t)]
     lib.zkl_step_proof_digest.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_void_p]
+    lib.zkl_children_root.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint32, C.c_void_p]
     lib.zkl_hip_lde.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]
     _lib = lib
     return lib
@@ -177,6 +178,58 @@ def step_proof_encode(pi: AirPublicInputs, info: StepInfo, inner: bytes) -> byte
     data = C.string_at(out, ln.value)
     lib.zkl_hip_free(out)
     return data
+
+
+def parse_step_proof(b: bytes) -> dict:
+    """Host mirror of StepProof::from_bytes (proof/step.rs:153-493): the fields of a ZKLSTP1
+    encoding, with the inner Winterfell proof bytes under "inner"."""
+    import struct
+    if len(b) < 7 or b[:7] != b"ZKLSTP1":
+        raise ValueError("invalid step proof magic tag")
+    off = 7
+
+    def take(k, what):
+        nonlocal off
+        if off + k > len(b):
+            raise ValueError(f"step proof truncated before {what}")
+        off += k
+        return b[off - k:off]
+
+    d = {"lambda_bits": struct.unpack("<I", take(4, "lambda_bits"))[0], "suite_id": take(32, "suite_id"),
+         "program_id": take(32, "program_id"), "program_commitment": take(32, "program_commitment"),
+         "merkle_root": take(32, "merkle_root"), "feature_mask": struct.unpack("<Q", take(8, "feature_mask"))[0]}
+    args = []
+    for _ in range(struct.unpack("<I", take(4, "main_args length"))[0]):
+        tag = take(1, "VmArg tag")[0]
+        if tag > 2:
+            raise ValueError("invalid VmArg tag in step proof encoding")
+        args.append((tag, take({0: 8, 1: 16, 2: 32}[tag], "VmArg")))
+    d["main_args"] = args
+    d["vm_usage_mask"] = struct.unpack("<I", take(4, "vm_usage_mask"))[0]
+    d["ram_delta_clk_bits"] = struct.unpack("<I", take(4, "ram_delta_clk_bits"))[0]
+    d["rom_acc"] = [take(32, "rom_acc") for _ in range(3)]
+    d["segment_index"] = struct.unpack("<I", take(4, "segment_index"))[0]
+    d["segments_total"] = struct.unpack("<I", take(4, "segments_total"))[0]
+    for f in ("pc_init", "state_in_hash", "state_out_hash", "ram_gp_unsorted_in", "ram_gp_unsorted_out",
+              "ram_gp_sorted_in", "ram_gp_sorted_out"):
+        d[f] = take(32, f)
+    d["rom_s_in"] = [take(32, "rom_s_in") for _ in range(3)]
+    d["rom_s_out"] = [take(32, "rom_s_out") for _ in range(3)]
+    d["inner"] = take(struct.unpack("<I", take(4, "inner proof length"))[0], "inner proof bytes")
+    if d["segments_total"] <= 1:  # new_single_segment (step.rs:413-432)
+        d["segment_index"], d["segments_total"] = 0, 1
+    return d
+
+
+def children_root(suite_id: bytes, digests, root_traces) -> bytes:
+    """agg::child::children_root_from_compact (agg/child.rs:853-895) over (step digest,
+    zl1 root_trace) pairs of the children."""
+    lib = load_library()
+    out = (C.c_uint8 * 32)()
+    rc = lib.zkl_children_root(bytes(suite_id), b"".join(digests), b"".join(root_traces), len(digests), out)
+    if rc:
+        raise ZklError(rc, lib.zkl_hip_last_error(None).decode())
+    return bytes(out)
 
 
 def step_proof_digest(step: bytes):

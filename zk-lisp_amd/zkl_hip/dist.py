@@ -76,6 +76,36 @@ def gather_to_root(obj):
     return out
 
 
+def collect_step_proofs(step_bytes):
+    """Aggregation hand-off: every rank contributes the ZKLSTP1 encodings of
+    the step proofs it produced; rank 0 receives all of them, decodes each one
+    (StepProof::from_bytes field order, proof/step.rs:153-493), orders them by segment
+    index and checks the boundary chain the aggregation AIR consumes (state_out_hash of
+    segment i == state_in_hash of segment i+1) and the step digests (digest.rs:16-68).
+    Returns the ordered list of dicts on rank 0, None elsewhere.  The payload is a few
+    hundred KB per segment, so it travels over the gloo control plane as host bytes."""
+    from . import parse_step_proof, step_proof_digest
+    got = gather_to_root(list(step_bytes))
+    if got is None:
+        return None
+    steps = []
+    for per_rank in got:
+        for b in per_rank:
+            d = parse_step_proof(b)
+            d["digest"], d["root_trace"] = step_proof_digest(b)
+            d["bytes"] = len(b)
+            steps.append(d)
+    steps.sort(key=lambda d: d["segment_index"])
+    total = steps[0]["segments_total"] if steps else 0
+    if [d["segment_index"] for d in steps] != list(range(len(steps))) or (total > 1 and total != len(steps)):
+        raise ValueError("step proofs do not cover segments 0..n-1 exactly once")
+    for a, b in zip(steps, steps[1:]):
+        if a["state_out_hash"] != b["state_in_hash"]:
+            raise ValueError(f"segment {b['segment_index']}: state_in_hash does not continue segment "
+                             f"{a['segment_index']}")
+    return steps
+
+
 def shutdown():
     global _dist
     if _dist is not None:
