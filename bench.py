@@ -100,6 +100,28 @@ def cpu_baseline(log_n_sample, log_n_target, threads):
     }
 
 
+def c5_single(zkl_hip, device, log_n):
+    """BASELINE configs[4] shape on one GPU: one synthetic 2^log_n-row segment (blowup 16,
+    q 64, grind 16, partitions (16,16) at 2^20 rows), trace resident in HBM; on 8 GPUs each
+    rank proves its own segment (replicas).  One warm-up proof, one timed.
+    Returns (ms per proof, proof bytes)."""
+    n = 1 << log_n
+    ctx = zkl_hip.Context(device)
+    t, pi, w = zkl_hip.synth_vm_segment(0x5EED0C05, log_n)
+    d = ctx.alloc(w * n * 16)
+    ctx.upload(d, t, w * n * 16)
+    del t
+    o = zkl_hip.proof_options(w, n)
+    ctx.prove_segment_device(d, w, n, pi, o)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    proof = ctx.prove_segment_device(d, w, n, pi, o)
+    ms = (time.perf_counter() - t0) * 1e3
+    ctx.free(d)
+    ctx.close()
+    return ms, len(proof)
+
+
 def c3_pipeline(zkl_hip, device, log_n, n_segments, inflight, reps=1):
     """BASELINE configs[2] shape: n_segments distinct 2^log_n-row segments proved on one GPU
     with `inflight` contexts (one HIP stream each) in host threads, so one segment's
@@ -164,6 +186,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c3-segments", type=int, default=8, help="segments for the configs[2] pipeline line (0: skip)")
     ap.add_argument("--c3-inflight", type=str, default="1,2,4", help="contexts in flight to try for configs[2]")
+    ap.add_argument("--c5-log-n", type=int, default=20, help="rows (log2) of the configs[4] single-segment line (0: skip)")
     args = ap.parse_args()
 
     # Only the result line goes to stdout: native libraries (gloo prints "[Gloo] Rank ..."
@@ -312,6 +335,16 @@ def main():
                 "config": f"BASELINE configs[2] shape: {args.c3_segments} distinct synthetic 2^{log_n}-row segments on 1 GPU",
                 "segment_proofs_per_s_by_inflight": c3, "best_inflight": int(kbest), "value": c3[kbest],
                 "unit": "segment-proofs/s"}
+        if world == 1 and args.c5_log_n > 0:
+            try:
+                ms5, pb5 = c5_single(zkl_hip, device, args.c5_log_n)
+                out["c5_single_segment"] = {
+                    "config": f"BASELINE configs[4] shape on one GPU: one synthetic 2^{args.c5_log_n}-row segment, "
+                              "blowup 16, q 64, grind 16 (each of the 8 GPUs proves its own)",
+                    "ms_per_proof": round(ms5, 1), "proof_bytes": pb5,
+                    "rows_per_s": round((1 << args.c5_log_n) / ms5 * 1e3)}
+            except Exception as e:  # reported, never fatal for the headline number
+                out["c5_single_segment"] = {"error": str(e)}
         if world == 1 and not args.no_cpu_baseline:
             try:
                 th = args.cpu_threads or min(16, os.cpu_count() or 1)
