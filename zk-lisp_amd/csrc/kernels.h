@@ -109,7 +109,8 @@ struct ProofConsts {
 };
 void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab,
                             const fe* d_bm /* (n_bcols + 1) x ce */, const CeParams& p, ProofConsts* dK,
-                            bool pose_block, bool ram_merkle, fe* d_out, hipStream_t s);
+                            bool pose_block, bool ram_merkle, fe* d_xinv /* ce scratch */, fe* d_out,
+                            hipStream_t s);
 // boundary vectors: vec[slot*n + step] = beta_a ; wv[s] = sum beta_a*value_a over assertions at step s
 void launch_boundary_scatter(const uint32_t* d_slot, const uint32_t* d_step, const fe* d_beta, size_t n_assert,
                              size_t n, fe* d_vecs, hipStream_t s);
@@ -136,7 +137,7 @@ struct DeepParams {
   fe z, zg, sz, szg;
 };
 void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p,
-                 const ProofConsts* dK, fe* d_out, hipStream_t s);
+                 const ProofConsts* dK, fe* d_dinv /* N scratch */, fe* d_out, hipStream_t s);
 void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s);
 // alpha read from device memory (written by launch_fri_coin)
 void launch_fri_fold(const fe* d_ev, size_t Nd, const fe* d_alpha, const fe* d_iroots, size_t Ntab, fe* d_out,

@@ -1050,7 +1050,8 @@ template <bool POSE, bool RM>
 __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restrict__ lde, const fe* __restrict__ roots,
                                                               int roots_shift, const fe* __restrict__ pertab,
                                                               const fe* __restrict__ bm,
-                                                              const ProofConsts* __restrict__ K, fe* __restrict__ out) {
+                                                              const ProofConsts* __restrict__ K,
+                                                              const fe* __restrict__ xinv, fe* __restrict__ out) {
   const AirDevice& c_air = K->air;
   const CeParams& c_ce = K->ce;
   const size_t ce = c_ce.ce, N = c_ce.N;
@@ -1070,7 +1071,7 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
   // p_last = L_{n-1}(x) = g^(n-1)/n * (x^n - 1) / (x - g^(n-1))
   fe x_gl = fe_sub_sel(x, c_ce.gl);
   fe xn_m1 = c_ce.xn_m1[i % blow];
-  fe p_last = fe_mul(fe_mul(c_ce.lagr, xn_m1), fe_inv(x_gl));
+  fe p_last = fe_mul(fe_mul(c_ce.lagr, xn_m1), xinv[i]);  // xinv[i] = 1 / (x - g^(n-1))
   fe s_low = fe_mul(p_last, p_map);
   fe g_carry = fe_add_sel(p_map, fe_sub_sel(p_pad, p_pad_last));
   for (int j = 0; j < 26; j++) g_carry = fe_add_sel(g_carry, per[1 + j]);
@@ -1379,20 +1380,52 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
   out[i] = fe_mul(v, xn_inv);
 }
 
+// out[i] = 1 / ((x_i - a1) (x_i - a2)^two) over the coset x_i = 3 w_M^i (w_M^i =
+// roots[i << shift]): each thread inverts INV_PTS points T apart with one field inversion
+// (Montgomery's trick), instead of one ~250-multiplication Fermat inversion per point.
+constexpr int INV_PTS = 16;
+__global__ __launch_bounds__(256) void coset_inv_kernel(const fe* __restrict__ roots, int shift, fe a1, fe a2, int two,
+                                                        fe* __restrict__ out) {
+  const size_t T = (size_t)gridDim.x * blockDim.x;
+  const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  fe den[INV_PTS], pre[INV_PTS];
+#pragma unroll
+  for (int k = 0; k < INV_PTS; k++) {
+    const fe x = fe_mul(fe{3, 0}, roots[(i0 + k * T) << shift]);
+    fe d = fe_sub(x, a1);
+    if (two) d = fe_mul(d, fe_sub(x, a2));
+    den[k] = d;
+    pre[k] = k ? fe_mul(pre[k - 1], d) : d;
+  }
+  fe inv = fe_inv(pre[INV_PTS - 1]);
+#pragma unroll
+  for (int k = INV_PTS - 1; k > 0; k--) {
+    out[i0 + k * T] = fe_mul(inv, pre[k - 1]);
+    inv = fe_mul(inv, den[k]);
+  }
+  out[i0] = inv;
+}
+static void launch_coset_inv(const fe* d_roots, int shift, size_t M, fe a1, fe a2, int two, fe* d_out, hipStream_t s) {
+  // M is a power of two >= INV_PTS
+  const size_t threads = std::min<size_t>(256, M / INV_PTS);
+  coset_inv_kernel<<<(unsigned)(M / (threads * INV_PTS)), (unsigned)threads, 0, s>>>(d_roots, shift, a1, a2, two, d_out);
+}
+
 void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab, const fe* d_bm,
-                            const CeParams& p, ProofConsts* dK, bool pose_block, bool ram_merkle, fe* d_out,
+                            const CeParams& p, ProofConsts* dK, bool pose_block, bool ram_merkle, fe* d_xinv, fe* d_out,
                             hipStream_t s) {
   (void)hipMemcpyAsync(&dK->ce, &p, sizeof p, hipMemcpyHostToDevice, s);
   int shift = ilog2s(Ntab) - ilog2s(p.ce);
+  launch_coset_inv(d_roots, shift, p.ce, p.gl, fe_zero(), 0, d_xinv, s);  // 1 / (x - g^(n-1))
   const unsigned grid = (unsigned)((p.ce + 255) / 256);
   if (pose_block && ram_merkle)
-    constraint_eval_kernel<true, true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_out);
+    constraint_eval_kernel<true, true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out);
   else if (pose_block)
-    constraint_eval_kernel<true, false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_out);
+    constraint_eval_kernel<true, false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out);
   else if (ram_merkle)
-    constraint_eval_kernel<false, true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_out);
+    constraint_eval_kernel<false, true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out);
   else
-    constraint_eval_kernel<false, false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_out);
+    constraint_eval_kernel<false, false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out);
 }
 
 __global__ void boundary_scatter_kernel(const uint32_t* slot, const uint32_t* step, const fe* beta, size_t na, size_t n,
@@ -1474,7 +1507,8 @@ __device__ __forceinline__ fe limbs_canon(const uint32_t l[5]) {
 
 __global__ __launch_bounds__(256) void deep_kernel(const fe* __restrict__ lde, const fe* __restrict__ clde,
                                                    const fe* __restrict__ roots, int shift, DeepParams p,
-                                                   const ProofConsts* __restrict__ K, fe* out) {
+                                                   const ProofConsts* __restrict__ K, const fe* __restrict__ dinv,
+                                                   fe* out) {
   const size_t T = (size_t)gridDim.x * blockDim.x;
   const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t col[DEEP_PTS][10];
@@ -1505,37 +1539,27 @@ __global__ __launch_bounds__(256) void deep_kernel(const fe* __restrict__ lde, c
       }
     }
   }
-  fe num[DEEP_PTS], den[DEEP_PTS];
+  // 1 / ((x - z)(x - zg)) comes from coset_inv_kernel (x is never z or zg: z is drawn
+  // outside the LDE domain, as Winterfell requires)
 #pragma unroll
   for (int k = 0; k < DEEP_PTS; k++) {
     uint32_t l[5];
     redc(col[k], l);
     const fe sv = limbs_canon(l);
-    const fe x = fe_mul(fe{3, 0}, roots[(i0 + k * T) << shift]);
+    const size_t i = i0 + k * T;
+    const fe x = fe_mul(fe{3, 0}, roots[i << shift]);
     const fe d1 = fe_sub(x, p.z), d2 = fe_sub(x, p.zg);
-    num[k] = fe_add(fe_mul(fe_sub(sv, p.sz), d2), fe_mul(fe_sub(sv, p.szg), d1));
-    den[k] = fe_mul(d1, d2);
+    const fe num = fe_add(fe_mul(fe_sub(sv, p.sz), d2), fe_mul(fe_sub(sv, p.szg), d1));
+    out[i] = fe_mul(num, dinv[i]);
   }
-  // batch inversion of the DEEP_PTS denominators (x is never z or zg: z is drawn outside
-  // the LDE domain, as Winterfell requires)
-  fe pre[DEEP_PTS];
-  pre[0] = den[0];
-#pragma unroll
-  for (int k = 1; k < DEEP_PTS; k++) pre[k] = fe_mul(pre[k - 1], den[k]);
-  fe inv = fe_inv(pre[DEEP_PTS - 1]);
-#pragma unroll
-  for (int k = DEEP_PTS - 1; k > 0; k--) {
-    out[i0 + k * T] = fe_mul(num[k], fe_mul(inv, pre[k - 1]));
-    inv = fe_mul(inv, den[k]);
-  }
-  out[i0] = fe_mul(num[0], inv);
 }
 void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p,
-                 const ProofConsts* dK, fe* d_out, hipStream_t s) {
+                 const ProofConsts* dK, fe* d_dinv, fe* d_out, hipStream_t s) {
+  launch_coset_inv(d_roots, ilog2s(Ntab) - ilog2s(p.N), p.N, p.z, p.zg, 1, d_dinv, s);
   // N is a power of two >= 64: every thread gets exactly DEEP_PTS points
   const size_t threads = std::min<size_t>(256, p.N / DEEP_PTS);
   deep_kernel<<<(unsigned)(p.N / (threads * DEEP_PTS)), (unsigned)threads, 0, s>>>(
-      d_lde, d_clde, d_roots, ilog2s(Ntab) - ilog2s(p.N), p, dK, d_out);
+      d_lde, d_clde, d_roots, ilog2s(Ntab) - ilog2s(p.N), p, dK, d_dinv, d_out);
 }
 
 // FRI layer leaves: hash_elements([e_i, e_{i+Nd/2}]) (FriProver::build_layer, folding 2)

@@ -135,6 +135,7 @@ struct zkl_ctx {
   // work buffers
   DBuf trace, coef, lde, parts, tree, ce, bvec, bm, clde, ctree, deep, draws, pw, oodv, asl, ast, asv, ars;
   DBuf fri_ev, fri_tree, best, gaddr, gout, flag;
+  DBuf xinv;  // batch-inverted coset denominators (constraint evaluation, DEEP)
   DBuf kconst;  // ProofConsts of the proof in flight on this context
   DBuf fri_coin;  // device transcript of the FRI layers: seed, alpha, layer roots
   size_t pert_key_n = 0, pert_key_ce = 0;
@@ -434,8 +435,9 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->ce.ensure(ce * sizeof(fe));
   {
     KScope k(C, KF_CEVAL);
+    C->xinv.ensure(std::max(ce, N) * sizeof(fe));
     launch_constraint_eval(C->lde.f(), roots, Ntab, C->pertab.f(), C->bm.f(), cp, dK, air.dev.pose_block != 0,
-                           (air.dev.ram_block | air.dev.merkle_block) != 0, C->ce.f(), s);
+                           (air.dev.ram_block | air.dev.merkle_block) != 0, C->xinv.f(), C->ce.f(), s);
   }
   T.mark(3);
 
@@ -539,7 +541,8 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->deep.ensure(N * sizeof(fe));
   {
     KScope k(C, KF_DEEP);
-    launch_deep(C->lde.f(), C->clde.f(), roots, Ntab, dp, dK, C->deep.f(), s);
+    C->xinv.ensure(N * sizeof(fe));
+    launch_deep(C->lde.f(), C->clde.f(), roots, Ntab, dp, dK, C->xinv.f(), C->deep.f(), s);
   }
   T.mark(6);
 
