@@ -513,3 +513,26 @@ def test_lde_lazy_ntt_matches_canonical(gpu_ctx, ncols, log_n, blow):
         for d in (d_v, d_c, d_l):
             gpu_ctx.free(d)
     assert outs[0] == outs[1]
+
+
+def test_full_size_proof_independent_of_kernel_forms(gpu_ctx):
+    """configs[1] shape (2^16 rows, blowup 16, q 64, grind 16): the proof bytes are the same
+    with the matrix-core or the lane-group permutation on every level and with the lazy or
+    the canonical DIT NTT — each form is checked against the others at full size."""
+    import zkl_hip
+    lib = zkl_hip.load_library()
+    n = 1 << 16
+    t, pi, w = zkl_hip.synth_vm_segment(0x5EEDF00D, 16)
+    opts = zkl_hip.proof_options(w, n)
+    proofs = {}
+    try:
+        for name, engine, min_items, lazy in (("default", 1, 1 << 14, 1), ("lane", 0, 1 << 14, 1),
+                                              ("all_mfma", 1, 32, 1), ("canonical_ntt", 1, 1 << 14, 0)):
+            assert lib.zkl_hip_set_hash_policy(engine, min_items) == 0
+            assert lib.zkl_hip_set_ntt_mode(lazy) == 0
+            proofs[name] = gpu_ctx.prove_segment(t, w, n, pi, opts)
+    finally:
+        lib.zkl_hip_set_hash_policy(1, 1 << 14)
+        lib.zkl_hip_set_ntt_mode(1)
+    ref = proofs["default"]
+    assert all(p == ref for p in proofs.values()), [k for k, p in proofs.items() if p != ref]
