@@ -146,7 +146,9 @@ int zkl_hip_prove_segment_device(zkl_ctx* ctx, const void* d_trace, uint32_t wid
  * stage marks not covered by device work, [2] the whole call.  Returns number written. */
 int zkl_hip_host_times(const zkl_ctx* ctx, double* out_ms, int max_n);
 
-/* Stage timings (ms) of the last proof on ctx; returns number written. */
+/* Stage timings (ms) of the last proof on ctx; returns number written.  Recorded only for
+ * proofs run with zkl_hip_set_kernel_timing(ctx, 2) (zeros otherwise: each stage event
+ * costs queue time on the proof stream). */
 int zkl_hip_stage_times(const zkl_ctx* ctx, double* out_ms, int max_n);
 
 /* Per-kernel-family device time of the last proof, measured with HIP events on the
@@ -155,7 +157,8 @@ int zkl_hip_stage_times(const zkl_ctx* ctx, double* out_ms, int max_n);
 #define ZKL_NUM_KFAMILIES 9
 int zkl_hip_kernel_times(const zkl_ctx* ctx, double* out_ms, int* out_launches, int max_n, const char** names);
 /* Which kernel families zkl_hip_kernel_times covers for the following proofs: 0 none,
- * 1 the trace row hash only (default: every bracket costs ~10 us of queue time), 2 all. */
+ * 1 the trace row hash only (default: every bracket costs ~10 us of queue time), 2 all
+ * families and the stage boundaries of zkl_hip_stage_times. */
 int zkl_hip_set_kernel_timing(zkl_ctx* ctx, int mode);
 
 /* ---- device memory (the library's own HIP runtime; callers need no torch) --- */

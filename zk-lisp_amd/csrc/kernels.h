@@ -136,8 +136,10 @@ struct DeepParams {
   uint32_t W, C;
   fe z, zg, sz, szg;
 };
+// d_dinv[i] = 1/((x_i - z)(x_i - zg)) over the LDE coset x_i = 3*w_N^i (launch before launch_deep)
+void launch_deep_denoms(const fe* d_roots, size_t Ntab, size_t N, fe z, fe zg, fe* d_dinv, hipStream_t s);
 void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p,
-                 const ProofConsts* dK, fe* d_dinv /* N scratch */, fe* d_out, hipStream_t s);
+                 const ProofConsts* dK, const fe* d_dinv /* from launch_deep_denoms */, fe* d_out, hipStream_t s);
 void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s);
 // alpha read from device memory (written by launch_fri_coin)
 void launch_fri_fold(const fe* d_ev, size_t Nd, const fe* d_alpha, const fe* d_iroots, size_t Ntab, fe* d_out,

@@ -1553,9 +1553,12 @@ __global__ __launch_bounds__(256) void deep_kernel(const fe* __restrict__ lde, c
     out[i] = fe_mul(num, dinv[i]);
   }
 }
+void launch_deep_denoms(const fe* d_roots, size_t Ntab, size_t N, fe z, fe zg, fe* d_dinv, hipStream_t s) {
+  launch_coset_inv(d_roots, ilog2s(Ntab) - ilog2s(N), N, z, zg, 1, d_dinv, s);
+}
+
 void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p,
-                 const ProofConsts* dK, fe* d_dinv, fe* d_out, hipStream_t s) {
-  launch_coset_inv(d_roots, ilog2s(Ntab) - ilog2s(p.N), p.N, p.z, p.zg, 1, d_dinv, s);
+                 const ProofConsts* dK, const fe* d_dinv, fe* d_out, hipStream_t s) {
   // N is a power of two >= 64: every thread gets exactly DEEP_PTS points
   const size_t threads = std::min<size_t>(256, p.N / DEEP_PTS);
   deep_kernel<<<(unsigned)(p.N / (threads * DEEP_PTS)), (unsigned)threads, 0, s>>>(

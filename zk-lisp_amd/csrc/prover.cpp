@@ -62,6 +62,25 @@ struct DBuf {
   ~DBuf() { if (p) (void)hipFree(p); }
 };
 
+// Pinned host staging: copies from/to it are asynchronous DMA that neither blocks the host
+// until the stream drains nor goes through the runtime's pageable bounce buffers.
+struct HBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t b) {
+    if (b <= bytes) return;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    b += b / 4;  // sizes vary a little from proof to proof (query count, assertions)
+    HIPCHECK(hipHostMalloc(&p, b, hipHostMallocDefault));
+    bytes = b;
+  }
+  template <class T>
+  T* at(size_t off = 0) const { return (T*)((char*)p + off); }
+  ~HBuf() { if (p) (void)hipHostFree(p); }
+};
+
 // ------------------------------------------------------------------ Fiat-Shamir coin
 // DefaultRandomCoin<PoseidonHasher> [WF-recall]; order pinned by agg/fs.rs:67-237.
 struct Coin {
@@ -75,48 +94,72 @@ struct Coin {
 struct Bytes {
   std::vector<uint8_t> v;
   void u8(uint8_t x) { v.push_back(x); }
-  void u64(uint64_t x) { for (int i = 0; i < 8; i++) v.push_back((uint8_t)(x >> (8 * i))); }
+  void raw(const void* p, size_t n) {
+    const size_t o = v.size();
+    v.resize(o + n);
+    memcpy(v.data() + o, p, n);
+  }
+  void u64(uint64_t x) {  // little-endian host (x86-64 / gfx950 hosts)
+    raw(&x, 8);
+  }
   void usize(uint64_t x) {  // winter-utils write_usize (vint64)
     int lz = x ? __builtin_clzll(x) : 64;
     int l = (lz > 0 ? lz - 1 : 0) / 7;
     int len = 9 - std::min(l, 8);
     if (len == 9) { u8(0); u64(x); return; }
     uint64_t enc = ((x << 1) | 1) << (len - 1);
-    for (int i = 0; i < len; i++) v.push_back((uint8_t)(enc >> (8 * i)));
+    raw(&enc, (size_t)len);
   }
-  void felem(fe x) { u64(x.lo); u64(x.hi); }
-  void digest(fe x) { felem(x); for (int i = 0; i < 16; i++) v.push_back(0); }
-  void vec(const Bytes& b) { usize(b.v.size()); v.insert(v.end(), b.v.begin(), b.v.end()); }
+  void felem(fe x) {
+    const uint64_t w[2] = {x.lo, x.hi};
+    raw(w, 16);
+  }
+  void digest(fe x) {
+    const uint64_t w[4] = {x.lo, x.hi, 0, 0};
+    raw(w, 32);
+  }
+  void vec(const Bytes& b) { usize(b.v.size()); raw(b.v.data(), b.v.size()); }
 };
 
 // MerkleTree::prove_batch node-index plan (winter-crypto 0.13, [WF-recall]):
 // returns, per normalized leaf pair, the list of tree-node indices whose digests go in.
 // Leaves are tree nodes n+i.
-std::vector<std::vector<uint64_t>> batch_plan(size_t n_leaves, const std::vector<size_t>& idx) {
-  int depth = ilog2(n_leaves);
-  std::vector<size_t> norm;
-  for (size_t i : idx) norm.push_back(i & ~(size_t)1);
+struct Plan {
+  std::vector<uint64_t> node;  // the lists back to back
+  std::vector<uint32_t> len;   // entries per list
+};
+Plan batch_plan(size_t n_leaves, const std::vector<size_t>& idx) {
+  const int depth = ilog2(n_leaves);
+  std::vector<size_t> norm(idx.size()), req(idx);
+  for (size_t k = 0; k < idx.size(); k++) norm[k] = idx[k] & ~(size_t)1;
   std::sort(norm.begin(), norm.end());
   norm.erase(std::unique(norm.begin(), norm.end()), norm.end());
-  std::set<size_t> req(idx.begin(), idx.end());
-  std::vector<std::vector<uint64_t>> lists(norm.size());
-  std::vector<size_t> next;
-  for (size_t k = 0; k < norm.size(); k++) {
+  std::sort(req.begin(), req.end());
+  // list k takes at most two leaves and one node per level: fixed-stride scratch, compacted
+  const size_t L = norm.size(), stride = (size_t)depth + 2;
+  std::vector<uint64_t> tmp(L * stride);
+  std::vector<uint32_t> cnt(L, 0);
+  std::vector<size_t> cur(L), next;
+  next.reserve(L);
+  for (size_t k = 0; k < L; k++) {
     for (size_t j = norm[k]; j < norm[k] + 2; j++)
-      if (!req.count(j)) lists[k].push_back(n_leaves + j);
-    next.push_back((norm[k] + n_leaves) >> 1);
+      if (!std::binary_search(req.begin(), req.end(), j)) tmp[k * stride + cnt[k]++] = n_leaves + j;
+    cur[k] = (norm[k] + n_leaves) >> 1;
   }
   for (int lvl = 1; lvl < depth; lvl++) {
-    std::vector<size_t> cur = next;
     next.clear();
     for (size_t i = 0; i < cur.size(); i++) {
       size_t sib = cur[i] ^ 1;
       if (i + 1 < cur.size() && cur[i + 1] == sib) i++;
-      else lists[i].push_back(sib);
+      else tmp[i * stride + cnt[i]++] = sib;
       next.push_back(sib >> 1);
     }
+    cur.swap(next);
   }
-  return lists;
+  Plan P;
+  P.len = cnt;
+  for (size_t k = 0; k < L; k++) P.node.insert(P.node.end(), tmp.begin() + k * stride, tmp.begin() + k * stride + cnt[k]);
+  return P;
 }
 
 }  // namespace
@@ -138,6 +181,11 @@ struct zkl_ctx {
   DBuf xinv;  // batch-inverted coset denominators (constraint evaluation, DEEP)
   DBuf kconst;  // ProofConsts of the proof in flight on this context
   DBuf fri_coin;  // device transcript of the FRI layers: seed, alpha, layer roots
+  HBuf h_asrt, h_ood, h_addr, h_gv;  // pinned staging: assertions, OOD partial sums, gather plan/values
+  hipStream_t aux = nullptr;         // copy stream: assertion upload overlapped with the trace commitment
+  hipEvent_t aux_ev = nullptr, hev = nullptr;
+  hipEvent_t stage_ev[ZKL_NUM_STAGES + 1] = {};
+  bool stage_ev_ready = false;
   size_t pert_key_n = 0, pert_key_ce = 0;
   // kernel-family timers (HIP events on `stream` around each launch group)
   std::vector<hipEvent_t> evpool;
@@ -246,24 +294,40 @@ void ensure_tables(zkl_ctx* C, size_t n, size_t N) {
   }
 }
 
+// Stage boundaries as HIP events on the proof stream.  Each record costs ~10 us of queue time,
+// so the inner boundaries are recorded only with zkl_hip_set_kernel_timing(ctx, 2); the first
+// and last (whole-proof device time) always are.  Events live in the context.
 struct StageTimer {
   zkl_ctx* C;
-  std::vector<hipEvent_t> ev;
-  explicit StageTimer(zkl_ctx* c) : C(c) {
-    ev.resize(ZKL_NUM_STAGES + 1);
-    for (auto& e : ev) (void)hipEventCreate(&e);
+  hipEvent_t* ev;
+  bool inner;
+  explicit StageTimer(zkl_ctx* c) : C(c), ev(c->stage_ev), inner(c->ktiming == 2) {
+    if (!C->stage_ev_ready) {
+      for (int i = 0; i <= ZKL_NUM_STAGES; i++) HIPCHECK(hipEventCreate(&C->stage_ev[i]));
+      C->stage_ev_ready = true;
+    }
   }
-  void mark(int i) { (void)hipEventRecord(ev[i], C->stream); }
+  void mark(int i) {
+    if (inner || i == 0 || i == ZKL_NUM_STAGES) (void)hipEventRecord(ev[i], C->stream);
+  }
   void finish() {
     (void)hipEventSynchronize(ev[ZKL_NUM_STAGES]);
     for (int i = 0; i < ZKL_NUM_STAGES; i++) {
       float ms = 0;
-      (void)hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+      if (inner) (void)hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
       C->stage_ms[i] = ms;
     }
   }
-  ~StageTimer() { for (auto& e : ev) (void)hipEventDestroy(e); }
 };
+
+// ZKL_HOST_TRACE=1: host timestamps (us since the call) of the phases around host round trips
+static const bool g_host_trace = getenv("ZKL_HOST_TRACE") != nullptr;
+#define HT(label)                                                                                   \
+  do {                                                                                              \
+    if (g_host_trace)                                                                               \
+      fprintf(stderr, "[ht] %-24s %9.1f\n", label,                                                  \
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_call0).count()); \
+  } while (0)
 
 template <class T>
 void d2h(zkl_ctx* C, T* dst, const void* src, size_t bytes) {
@@ -363,8 +427,15 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     if (!slot_of.count(a.col)) { slot_of[a.col] = (uint32_t)bcols.size(); bcols.push_back(a.col); }
   if (bcols.size() > 64) throw InvalidArg("too many asserted columns");
   const uint32_t nb = (uint32_t)bcols.size();
-  std::vector<uint32_t> hslot(na), hstep(na), rowstart(n + 1, 0);
-  std::vector<fe> hval(na);
+  // assertion tables written straight into pinned memory and uploaded on the copy stream,
+  // so the DMA runs under the trace commitment instead of after it
+  const size_t off_st = na * 4, off_sv = (na * 8 + 15) & ~(size_t)15, off_rs = off_sv + na * sizeof(fe);
+  C->h_asrt.ensure(off_rs + (n + 1) * 4);
+  uint32_t* hslot = C->h_asrt.at<uint32_t>(0);
+  uint32_t* hstep = C->h_asrt.at<uint32_t>(off_st);
+  fe* hval = C->h_asrt.at<fe>(off_sv);
+  uint32_t* rowstart = C->h_asrt.at<uint32_t>(off_rs);
+  memset(rowstart, 0, (n + 1) * 4);
   for (size_t k = 0; k < na; k++) {
     hslot[k] = slot_of[air.assertions[k].col];
     hstep[k] = air.assertions[k].step;
@@ -373,14 +444,23 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   }
   for (size_t r = 0; r < n; r++) rowstart[r + 1] += rowstart[r];
   C->asl.ensure(na * 4); C->ast.ensure(na * 4); C->asv.ensure(na * sizeof(fe)); C->ars.ensure((n + 1) * 4);
-  HIPCHECK(hipMemcpyAsync(C->asl.p, hslot.data(), na * 4, hipMemcpyHostToDevice, s));
-  HIPCHECK(hipMemcpyAsync(C->ast.p, hstep.data(), na * 4, hipMemcpyHostToDevice, s));
-  HIPCHECK(hipMemcpyAsync(C->asv.p, hval.data(), na * sizeof(fe), hipMemcpyHostToDevice, s));
-  HIPCHECK(hipMemcpyAsync(C->ars.p, rowstart.data(), (n + 1) * 4, hipMemcpyHostToDevice, s));
+  if (!C->aux) {
+    HIPCHECK(hipStreamCreateWithFlags(&C->aux, hipStreamNonBlocking));
+    HIPCHECK(hipEventCreateWithFlags(&C->aux_ev, hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&C->hev, hipEventDisableTiming));
+  }
+  HIPCHECK(hipMemcpyAsync(C->asl.p, hslot, na * 4, hipMemcpyHostToDevice, C->aux));
+  HIPCHECK(hipMemcpyAsync(C->ast.p, hstep, na * 4, hipMemcpyHostToDevice, C->aux));
+  HIPCHECK(hipMemcpyAsync(C->asv.p, hval, na * sizeof(fe), hipMemcpyHostToDevice, C->aux));
+  HIPCHECK(hipMemcpyAsync(C->ars.p, rowstart, (n + 1) * 4, hipMemcpyHostToDevice, C->aux));
+  HIPCHECK(hipEventRecord(C->aux_ev, C->aux));
+  HIPCHECK(hipStreamWaitEvent(s, C->aux_ev, 0));
   C->bvec.ensure((size_t)(nb + 1) * n * sizeof(fe));
   C->bm.ensure((size_t)(nb + 1) * ce * sizeof(fe));
+  HT("air_built");
   fe troot;
   d2h(C, &troot, C->tree.f() + 1, sizeof(fe));
+  HT("troot");
   coin.reseed(troot);
   T.mark(2);
 
@@ -477,6 +557,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   T.mark(4);
 
   // ---- 4. OOD frame at z and z*g
+  HT("croot");
   fe z = coin.draw(), zg = fe_mul(z, g);
   C->pw.ensure(4 * n * sizeof(fe));
   fe* pw = C->pw.f();
@@ -501,8 +582,20 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     for (int j = 0; j < Cc; j++) b.off[j] = bitrev_u((uint32_t)j, loge);
     launch_ood(b, dood + n_otr, s);
   }
-  std::vector<fe> part(n_otr + n_ocp), hood(2 * ((size_t)W + Cc), fe_zero());
-  d2h(C, part.data(), dood, part.size() * sizeof(fe));
+  std::vector<fe> hood(2 * ((size_t)W + Cc), fe_zero());
+  C->h_ood.ensure((n_otr + n_ocp) * sizeof(fe));
+  const fe* part = C->h_ood.at<fe>();
+  HIPCHECK(hipMemcpyAsync(C->h_ood.p, dood, (n_otr + n_ocp) * sizeof(fe), hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipEventRecord(C->hev, s));
+  // the DEEP denominators depend on z only: the device computes them while the host sums the
+  // OOD partials and hashes them into the transcript
+  C->xinv.ensure(std::max(ce, N) * sizeof(fe));
+  {
+    KScope k(C, KF_DEEP);
+    launch_deep_denoms(roots, Ntab, N, z, zg, C->xinv.f(), s);
+  }
+  HT("ood_enqueued");
+  HIPCHECK(hipEventSynchronize(C->hev));
   // hood = t(z) [W] | t(zg) [W] | chat(z) [Cc] | chat(zg) [Cc]
   for (size_t pt = 0; pt < 2; pt++) {
     for (uint32_t c = 0; c < W; c++)
@@ -528,10 +621,12 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   T.mark(5);
 
   // ---- 5. DEEP composition coefficients (W trace, then C constraint) and evaluations
+  HT("ood_hashed");
   std::vector<fe> gam(W + Cc);
   launch_draws(coin.seed, coin.counter, W + Cc, C->draws.f(), s);
   coin.counter += W + Cc;
   d2h(C, gam.data(), C->draws.p, gam.size() * sizeof(fe));
+  HT("gam");
   upload_deep_coeffs(dK, gam.data(), (int)gam.size(), s);
   DeepParams dp{};
   dp.N = N; dp.W = W; dp.C = Cc; dp.z = z; dp.zg = zg;
@@ -541,7 +636,6 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->deep.ensure(N * sizeof(fe));
   {
     KScope k(C, KF_DEEP);
-    C->xinv.ensure(N * sizeof(fe));
     launch_deep(C->lde.f(), C->clde.f(), roots, Ntab, dp, dK, C->xinv.f(), C->deep.f(), s);
   }
   T.mark(6);
@@ -581,6 +675,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     launch_fri_coin(d_coin, tr + 1, d_coin + 2 + d, s);
     launch_fri_fold(layer_ev(d), Nd, d_coin + 1, iroots, Ntab, layer_ev(d + 1), s);
   }
+  HT("fri_enqueued");
   if (nl > 0) {
     std::vector<fe> cs(2 + (size_t)nl);
     d2h(C, cs.data(), d_coin, cs.size() * sizeof(fe));
@@ -604,11 +699,13 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   const size_t rlen = o.fri_remainder_max_degree + 1;
   std::vector<fe> rem(rlen);
   for (size_t k = 0; k < rlen; k++) rem[k] = rc[rlen - 1 - k];
+  HT("rem");
   fe rem_commit = H.hash_elements(rem.data(), rlen);
   coin.reseed(rem_commit);
   T.mark(7);
 
   // ---- 7. grinding: smallest nonce >= 1 (winterfell without `concurrent`)
+  HT("grind_start");
   uint64_t nonce = 0;
   C->best.ensure(8);
   if (o.grinding_factor == 0) {
@@ -628,27 +725,30 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   T.mark(8);
 
   // ---- 8. query positions: draw_integers(q, N, nonce), sort, dedup
+  HT("q_start");
   coin.seed = H.merge_with_int(coin.seed, nonce);
   coin.counter = 0;
   std::vector<fe> qd(o.num_queries);
   launch_draws(coin.seed, 0, o.num_queries, C->draws.f(), s);
   d2h(C, qd.data(), C->draws.p, qd.size() * sizeof(fe));
+  HT("q_drawn");
   std::vector<size_t> pos;
   for (auto& v : qd) pos.push_back((size_t)(v.lo & (N - 1)));
   std::sort(pos.begin(), pos.end());
   pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
   const size_t nq = pos.size();
 
+  HT("q_sorted");
   // gather plan: trace rows, comp rows, trace/comp tree nodes, FRI values + tree nodes
   std::vector<uint64_t> addrs;
   auto A = [&](const fe* p) { addrs.push_back((uint64_t)(uintptr_t)p); };
   for (size_t k = 0; k < nq; k++) for (uint32_t c = 0; c < W; c++) A(C->lde.f() + (size_t)c * N + pos[k]);
   for (size_t k = 0; k < nq; k++) for (int j = 0; j < Cc; j++) A(C->clde.f() + (size_t)j * N + pos[k]);
   auto tplan = batch_plan(N, pos);
-  for (auto& l : tplan) for (auto ix : l) A(C->tree.f() + ix);
-  for (auto& l : tplan) for (auto ix : l) A(C->ctree.f() + ix);
+  for (auto ix : tplan.node) A(C->tree.f() + ix);
+  for (auto ix : tplan.node) A(C->ctree.f() + ix);
   std::vector<std::vector<size_t>> fpos(nl);
-  std::vector<std::vector<std::vector<uint64_t>>> fplan(nl);
+  std::vector<Plan> fplan(nl);
   {
     std::vector<size_t> p = pos;
     size_t dsz = N;
@@ -659,17 +759,24 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
       fpos[d] = f;
       for (size_t y : f) { A(layer_ev(d) + y); A(layer_ev(d) + y + h); }
       fplan[d] = batch_plan(h, f);
-      for (auto& l : fplan[d]) for (auto ix : l) A(C->fri_tree.f() + tr_off[d] + ix);
+      for (auto ix : fplan[d].node) A(C->fri_tree.f() + tr_off[d] + ix);
       p = f;
       dsz = h;
     }
   }
-  C->gaddr.ensure(addrs.size() * 8);
-  C->gout.ensure(addrs.size() * sizeof(fe));
-  HIPCHECK(hipMemcpyAsync(C->gaddr.p, addrs.data(), addrs.size() * 8, hipMemcpyHostToDevice, s));
-  launch_gather((const uint64_t*)C->gaddr.p, addrs.size(), C->gout.f(), s);
-  std::vector<fe> gv(addrs.size());
-  d2h(C, gv.data(), C->gout.p, gv.size() * sizeof(fe));
+  HT("q_planned");
+  const size_t na_g = addrs.size();
+  C->gaddr.ensure((na_g + na_g / 4) * 8);
+  C->gout.ensure((na_g + na_g / 4) * sizeof(fe));
+  C->h_addr.ensure(na_g * 8);
+  C->h_gv.ensure(na_g * sizeof(fe));
+  memcpy(C->h_addr.p, addrs.data(), na_g * 8);
+  HIPCHECK(hipMemcpyAsync(C->gaddr.p, C->h_addr.p, na_g * 8, hipMemcpyHostToDevice, s));
+  launch_gather((const uint64_t*)C->gaddr.p, na_g, C->gout.f(), s);
+  HIPCHECK(hipMemcpyAsync(C->h_gv.p, C->gout.p, na_g * sizeof(fe), hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  HT("q_gathered");
+  const fe* gv = C->h_gv.at<fe>();
   size_t gi = 0;
 
   // ---- 9. Proof::to_bytes  [WF-recall layout, DESIGN.md §Proof bytes]
@@ -688,12 +795,12 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     cm.digest(rem_commit);
     P.vec(cm);
   }
-  auto emit_multiproof = [&](Bytes& b, const std::vector<std::vector<uint64_t>>& plan, int depth) {
+  auto emit_multiproof = [&](Bytes& b, const Plan& plan, int depth) {
     b.u8((uint8_t)depth);
-    b.u8((uint8_t)plan.size());
-    for (auto& l : plan) {
-      b.u8((uint8_t)l.size());
-      for (size_t k = 0; k < l.size(); k++) b.digest(gv[gi++]);
+    b.u8((uint8_t)plan.len.size());
+    for (uint32_t l : plan.len) {
+      b.u8((uint8_t)l);
+      for (uint32_t k = 0; k < l; k++) b.digest(gv[gi++]);
     }
   };
   Bytes tv, cv, tp, cpb;
@@ -726,7 +833,8 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   }
   P.u8(0);  // FriProof num_partitions (log2 of 1)
   P.u64(nonce);
-  if (gi != gv.size()) throw std::runtime_error("internal: gather plan mismatch");
+  if (gi != na_g) throw std::runtime_error("internal: gather plan mismatch");
+  HT("serialised");
   T.mark(9);
   T.mark(10);
   T.finish();
@@ -790,6 +898,14 @@ void zkl_hip_destroy(zkl_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamDestroy(c->stream);
+  if (c->stage_ev_ready)
+    for (auto& e : c->stage_ev) (void)hipEventDestroy(e);
+  if (c->aux) {
+    (void)hipStreamSynchronize(c->aux);
+    (void)hipStreamDestroy(c->aux);
+    (void)hipEventDestroy(c->aux_ev);
+    (void)hipEventDestroy(c->hev);
+  }
   delete c;
 }
 
