@@ -371,12 +371,6 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   StageTimer T(C);
   T.mark(0);
   C->host_ms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call0).count();
-  // ---- coin seed: Context::to_elements || AirPublicInputs::to_elements (agg/fs.rs:67-73)
-  std::vector<fe> seed_el = context_elements(W, n, o);
-  auto pie = pi_elements(pi);
-  seed_el.insert(seed_el.end(), pie.begin(), pie.end());
-  Coin coin{H.hash_elements(seed_el.data(), seed_el.size()), 0};
-
   // ---- 1. trace LDE (DefaultTraceLde::new): iNTT over <g>, coset LDE over 3*<w_N>
   C->coef.ensure((size_t)W * n * sizeof(fe));
   C->lde.ensure((size_t)W * N * sizeof(fe));
@@ -401,8 +395,14 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     KScope k(C, KF_MERKLE);
     launch_merkle(C->tree.f(), N, s);
   }
+  // ---- coin seed: Context::to_elements || AirPublicInputs::to_elements (agg/fs.rs:67-73),
+  // hashed on the host while the device runs the trace LDE and commitment queued above
+  std::vector<fe> seed_el = context_elements(W, n, o);
+  auto pie = pi_elements(pi);
+  seed_el.insert(seed_el.end(), pie.begin(), pie.end());
+  Coin coin{H.hash_elements(seed_el.data(), seed_el.size()), 0};
   // The AIR instance (layout, degrees, ~2.9e5 assertions at n = 2^16) is built on the host
-  // while the device runs the trace LDE and commitment queued above.
+  // meanwhile too.
   AirInstance air;
   {
     std::string e = build_air(pi, W, n, air);
