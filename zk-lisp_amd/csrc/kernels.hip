@@ -287,41 +287,54 @@ __device__ __forceinline__ fe pg_bcast(const PGroup& P, fe v, int src) {
 }
 
 // ---- wide lane groups (latency-bound levels) ------------------------------------------
-// 24 lanes per state: lane (e, h) owns state element e (both halves hold it) and the MDS
-// row-e constants of columns 6h..6h+5; each half sums six products and the halves add
-// their 64-bit column sums through LDS before the (redundant) REDC.  Two states per wave
-// (lanes 48..63 idle).  A round issues ~345 instead of ~518 instructions per lane, so a
-// permutation finishes ~1.5x sooner; used where a level has too few states to fill the
-// SIMDs (upper Merkle levels, small FRI layers, the FRI transcript).
-constexpr int PW_PER_WAVE = 2;
-constexpr int PW_GROUP_WORDS = 60 + 24 * 20;  // cubes [l][12] + partial columns [h*12+e][20]
-constexpr int PW_WAVE_WORDS = 3 * PW_GROUP_WORDS;
+// PW_SPLIT (2 or 4) lanes per state element: lane SPLIT*e + h owns element e (every lane of
+// the element holds it) and the MDS row-e constants of columns COLS*h .. COLS*h + COLS-1
+// (COLS = 12 / SPLIT).  Each lane sums its COLS products and reduces them (REDC is linear:
+// REDC(a) + REDC(b) == (a + b) R^-1 mod p, and each output is < p + 2^109 since R = 2^156
+// >> p, so the sum of four plus a round constant keeps limbs < 2^28.4, inside the bounds
+// mont_cube and redc assume); the lanes of an element add their reduced parts with DPP
+// quad permutes instead of a second LDS exchange.  One state per wave at SPLIT 4 (lanes
+// 48..63 idle), two at SPLIT 2.  Used where a level has too few states to fill the SIMDs
+// (upper Merkle levels, small FRI layers, the FRI transcript): one permutation's dependency
+// chain bounds those levels.
+#ifndef PW_SPLIT
+#define PW_SPLIT 4
+#endif
+static_assert(PW_SPLIT == 2 || PW_SPLIT == 4, "PW_SPLIT must be 2 or 4");
+constexpr int PW_COLS = 12 / PW_SPLIT;
+constexpr int PW_LANES = 12 * PW_SPLIT;
+constexpr int PW_PER_WAVE = 64 / PW_LANES;
+constexpr int PW_GROUP_WORDS = 60;  // cubes [l][12]
+constexpr int PW_WAVE_WORDS = (PW_PER_WAVE + 1) * PW_GROUP_WORDS;  // + the idle partial group
 
 struct PWGroup {
-  uint32_t m[6][5];  // MDS row e, columns 6h..6h+5 (Montgomery)
-  uint32_t* x;       // cubes: x[limb * 12 + e]
-  uint32_t* y;       // partial column sums: y[(h * 12 + e) * 20 + w]
+  uint32_t m[PW_COLS][5];  // MDS row e, columns COLS*h .. (Montgomery)
+  uint32_t* x;             // cubes: x[limb * 12 + e]
   int e, h, g;
 };
 
 __device__ __forceinline__ void pw_init(PWGroup& P, uint32_t* lds) {
   const int lane = (int)(threadIdx.x & 63);
-  P.g = lane / 24;
-  const int j24 = lane - 24 * P.g;
-  P.h = j24 / 12;
-  P.e = j24 - 12 * P.h;
+  P.g = lane / PW_LANES;
+  const int j = lane - PW_LANES * P.g;
+  P.e = min(j / PW_SPLIT, 11);
+  P.h = j % PW_SPLIT;
   P.x = lds + (threadIdx.x >> 6) * PW_WAVE_WORDS + P.g * PW_GROUP_WORDS;
-  P.y = P.x + 60;
 #pragma unroll
-  for (int k = 0; k < 6; k++)
+  for (int k = 0; k < PW_COLS; k++)
 #pragma unroll
-    for (int l = 0; l < 5; l++) P.m[k][l] = c_hm.mds[P.e][6 * P.h + k][l];
+    for (int l = 0; l < 5; l++) P.m[k][l] = c_hm.mds[P.e][PW_COLS * P.h + k][l];
+}
+
+// sum of v over the SPLIT lanes of this lane's element (DPP quad_perm [1,0,3,2], [2,3,0,1])
+__device__ __forceinline__ uint32_t pw_elem_sum(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+  if (PW_SPLIT == 4) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  return v;
 }
 
 __device__ __forceinline__ void pw_permute(PWGroup& P, uint32_t s[5]) {
   const uint32_t* rcp = &c_hm.rc[0][P.e][0];
-  uint4* ymine = reinterpret_cast<uint4*>(P.y + (P.h * 12 + P.e) * 20);
-  const uint4* yother = reinterpret_cast<const uint4*>(P.y + ((1 - P.h) * 12 + P.e) * 20);
 #pragma unroll 1
   for (int r = 0; r < 27; r++, rcp += 60) {
     uint32_t rc[5];
@@ -334,34 +347,19 @@ __device__ __forceinline__ void pw_permute(PWGroup& P, uint32_t s[5]) {
       for (int l = 0; l < 5; l++) P.x[l * 12 + P.e] = t[l];
     }
     wave_sync();
-    uint32_t tk[6][5];
+    uint32_t tk[PW_COLS][5];
 #pragma unroll
-    for (int l = 0; l < 5; l++) {
+    for (int l = 0; l < 5; l++)
 #pragma unroll
-      for (int q = 0; q < 3; q++) {
-        const uint2 w = *reinterpret_cast<const uint2*>(P.x + l * 12 + 6 * P.h + 2 * q);
-        tk[2 * q][l] = w.x;
-        tk[2 * q + 1][l] = w.y;
-      }
-    }
+      for (int k = 0; k < PW_COLS; k++) tk[k][l] = P.x[l * 12 + PW_COLS * P.h + k];
+    __builtin_amdgcn_wave_barrier();
     uint64_t col[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 6; k++) mac5(tk[k], P.m[k], col);
+    for (int k = 0; k < PW_COLS; k++) mac5(tk[k], P.m[k], col);
+    uint32_t part[5];
+    redc(col, part);
 #pragma unroll
-    for (int q = 0; q < 5; q++)
-      ymine[q] = make_uint4((uint32_t)col[2 * q], (uint32_t)(col[2 * q] >> 32), (uint32_t)col[2 * q + 1],
-                            (uint32_t)(col[2 * q + 1] >> 32));
-    wave_sync();
-#pragma unroll
-    for (int q = 0; q < 5; q++) {
-      const uint4 o = yother[q];
-      col[2 * q] += ((uint64_t)o.y << 32) | o.x;
-      col[2 * q + 1] += ((uint64_t)o.w << 32) | o.z;
-    }
-    __builtin_amdgcn_wave_barrier();
-    redc(col, s);
-#pragma unroll
-    for (int l = 0; l < 5; l++) s[l] += rc[l];
+    for (int l = 0; l < 5; l++) s[l] = pw_elem_sum(part[l]) + rc[l];
   }
 }
 
@@ -386,7 +384,7 @@ __device__ __forceinline__ fe pw_sponge(PWGroup& P, bool live, int nmsg, Loader 
 }
 
 __device__ __forceinline__ fe pw_bcast(const PWGroup& P, fe v, int src_e) {
-  const int from = 24 * P.g + src_e;
+  const int from = PW_LANES * P.g + PW_SPLIT * src_e;
   fe r;
   r.lo = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v.lo >> 32), from) << 32) | (uint32_t)__shfl((int)(uint32_t)v.lo, from);
   r.hi = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v.hi >> 32), from) << 32) | (uint32_t)__shfl((int)(uint32_t)v.hi, from);
@@ -524,7 +522,7 @@ __global__ __launch_bounds__(256) void merkle_level_wide_kernel(fe* nodes, size_
 // lvl/cnt, with a workgroup barrier between levels; waves without a live node skip the
 // permutation.  A launch per level would add ~10 us of dispatch latency to each of these
 // permutation-latency-bound levels.
-constexpr int TOP_WAVES = 4;
+constexpr int TOP_WAVES = 8 / PW_PER_WAVE;
 constexpr int TOP_SLOTS = TOP_WAVES * PW_PER_WAVE;  // 8
 __global__ __launch_bounds__(64 * TOP_WAVES) void merkle_top_kernel(fe* nodes, size_t lvl, int cnt) {
   __shared__ __align__(16) uint32_t pw_lds[TOP_WAVES * PW_WAVE_WORDS];
