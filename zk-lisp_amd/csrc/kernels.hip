@@ -404,7 +404,10 @@ static inline unsigned pw_blocks(size_t items) {
 
 // levels (and FRI layers) with at most this many states use the wide groups: up to one
 // wide wave per SIMD, where per-state latency rather than issue throughput bounds the level
-constexpr size_t PW_MAX_ITEMS = 2048;
+#ifndef PW_MAX_ITEMS_CFG
+#define PW_MAX_ITEMS_CFG 2048
+#endif
+constexpr size_t PW_MAX_ITEMS = PW_MAX_ITEMS_CFG;
 
 // Occupancy target of the lane-group kernels: 2 waves/SIMD lets the scheduler batch the 15
 // LDS reads of a round; 3 forces them to serialise on a shared register window.
