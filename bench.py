@@ -3,21 +3,37 @@
 
 Workload (BASELINE.json configs[1] shape): one synthetic VM segment of 65,536 rows x 204
 columns ({vm, rom} layout), blowup 16, q 64, grind 16, partitions (4, 16).  One step = one
-full segment proof (trace LDE, constraint evaluation, composition, DEEP, FRI, grinding,
-queries, Proof::to_bytes) with the trace already resident in HBM.
+full segment proof per rank (trace LDE, constraint evaluation, composition, DEEP, FRI,
+grinding, queries, Proof::to_bytes) with the trace already resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--segments S] [--dry-run]
 
-N > 1 is launched by torch.distributed.run, one rank per GPU; each rank proves its own
-segments (weak scaling, no data-path collective).  The barrier and the
-max-over-ranks timing (zkl_hip/dist.py) use torch.distributed's gloo backend: the
-prover's HIP runtime (/opt/rocm 7.2) owns the device, and loading torch's bundled ROCm
-runtime into the same process would create a second HIP runtime.
-Device synchronisation is zkl_hip_synchronize (hipDeviceSynchronize) on both sides.
+Ranks.  N > 1 runs one process per GPU.  Under torch.distributed.run (RANK / WORLD_SIZE set)
+this process is one rank and WORLD_SIZE must equal --gpus.  Started directly with --gpus N > 1
+and no WORLD_SIZE, this process is only a launcher: before touching any GPU it starts N child
+processes of itself with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT
+set, relays rank 0's JSON line and exits non-zero if any rank fails.  Rank r proves segment
+seed 0x5EED0001 + r on device LOCAL_RANK (ZKL_BENCH_DEVICE pins every rank to one device to
+rehearse N ranks on fewer GPUs; the JSON line then says so).  Weak scaling, no data-path
+collective; the barrier, max-over-ranks timing and the step-proof hand-off
+use torch.distributed's gloo backend on host memory (zkl_hip/dist.py).
+
+Parity.  Every rank hashes its last proof and compares it with the committed CPU-oracle
+golden of its segment (tests/golden/proof_2p16.json, make_proof_goldens.py); at N = 1 the
+cpu_baseline leg also proves the same segment on the oracle and compares the bytes.
+
+Other lines: configs[2] (8 distinct segments on one GPU, 1/2/4 contexts in flight), configs[3]
+shape (--segments S distinct segments sharded over the ranks, each rank pipelining its share,
+then the step-proof gather and children root on rank 0; default S = 8 x N when N > 1) and
+configs[4] (one 2^20-row segment).  Device synchronisation is zkl_hip_synchronize
+(hipDeviceSynchronize) on both sides of every timed region.
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,15 +42,9 @@ sys.path.insert(0, os.path.join(ROOT, "zk-lisp_amd"))
 
 METRIC = "segment-proofs/sec at 65536 rows, blowup=16; proof bytes bit-exact vs CPU ref"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU issue peak: one wave64 VALU instruction per quad-cycle per SIMD (SQ_ACTIVE_INST_VALU
-# counts one quad-cycle per instruction for this kernel's 64-bit integer mix), 256 CUs x 4
-# SIMDs x 2.4 GHz / 4
-VALU_ISSUE_PEAK_G = 256 * 4 * 2.4 / 4   # G wave-instructions/s
-# VALU wave-instructions per Poseidon permutation of the trace row hash, from
-# SQ_INSTS_VALU / permutations: matrix-core kernel hash_rows_pm_kernel<0> 1025
-# (profiles/r01/pmc_sq_pm.json; the MDS runs on v_mfma_i32_32x32x32_i8), lane-group kernel
-# hash_rows_kernel<0> 2617 (profiles/r01/pmc_sq_stagebench.json, ZKL_HASH_ENGINE=lane)
-VALU_INSTR_PER_PERM = {"mfma": 1025, "lane": 2617}
+SEED0 = 0x5EED0001             # segment seed of rank / segment 0
+GOLDEN = os.path.join(ROOT, "tests", "golden", "proof_2p16.json")
+VALU_MIX = os.path.join(ROOT, "profiles", "r02", "valu_mix.json")
 ROW_KERNEL = {"mfma": "hash_rows_pm_kernel<0>", "lane": "hash_rows_kernel<0>"}
 
 
@@ -43,7 +53,7 @@ def log(*a):
 
 
 def perm_model(n, W=204, C=7, blowup=16, parts=None, grind=16, n_tc=193, queries=64):
-    """Algorithmic Poseidon permutation count of one segment proof (DESIGN.md §Work model)."""
+    """Algorithmic Poseidon permutation count of one segment proof (DESIGN.md §5 work model)."""
     N = n * blowup
     if parts is None:
         parts = 16 if n >= 1 << 20 else 8 if n >= 1 << 18 else 4 if n >= 1 << 16 else 2 if n >= 1 << 14 else 1
@@ -70,36 +80,138 @@ def perm_model(n, W=204, C=7, blowup=16, parts=None, grind=16, n_tc=193, queries
 MULMODS_PER_PERM = 27 * (144 + 24)  # f128 multiplications of one permutation (12 cubes x 2 + 144 MDS)
 
 
-def cpu_baseline(log_n_sample, log_n_target, threads):
-    """Oracle (CPU restatement of the reference algorithm) on a bounded sample: one full proof
-    of the same synthetic segment family at 2^log_n_sample rows with `threads` OpenMP
-    threads (row hashing, Merkle levels, LDE columns, constraint evaluation, DEEP, grinding
-    in parallel), extrapolated to 2^log_n_target rows by the permutation-count work model."""
+def golden_sha(seed, log_n):
+    """sha256 of the oracle proof of segment `seed` at the headline options, if committed."""
+    if log_n != 16 or not os.path.exists(GOLDEN):
+        return None
+    for v in json.load(open(GOLDEN)).values():
+        if v["seed"] == seed and v["flags"] == 0 and v["log_n"] == log_n:
+            return v["sha256"]
+    return None
+
+
+def parity_of(proof, seed, log_n):
+    want = golden_sha(seed, log_n)
+    got = hashlib.sha256(proof).hexdigest()
+    return {"seed": hex(seed), "sha256": got, "golden": "match" if want == got else ("none" if want is None else "MISMATCH")}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads(requested):
+    if requested:
+        return requested
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return min(16, os.cpu_count() or 1)
+
+
+def cpu_baseline(log_n, threads, gpu_proof, log_n_target):
+    """Oracle (oracle/, the CPU restatement of the reference algorithm) proving the bench's own
+    segment (seed SEED0, same options) with `threads` OpenMP threads inside the one proof (row
+    hashing, Merkle levels, LDE columns, constraint evaluation, DEEP, grinding in parallel).
+    At log_n == log_n_target this is the measured CPU rate of the headline workload, and its
+    proof bytes are compared with the GPU proof of the same segment."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as orc
     orc.lib()
     orc.set_threads(threads)
-    n = 1 << log_n_sample
-    t, pi, w = orc.synth_segment(0x5EED0001, log_n_sample)
+    n = 1 << log_n
+    t, pi, w = orc.synth_segment(SEED0, log_n)
     opts = orc.default_options(w, n)
     t0 = time.perf_counter()
-    orc.prove(t, w, n, pi, opts)
+    proof = orc.prove(t, w, n, pi, opts)
     dt = time.perf_counter() - t0
+    stages = dict(zip(("trace_lde", "trace_commit", "evaluator", "constraint_commitment", "deep", "fri",
+                       "grind", "queries"), (round(x / 1e3, 3) for x in orc.last_times())))
     orc.set_threads(1)
-    ms, mt = perm_model(n), perm_model(1 << log_n_target)
-    per_target = dt * mt["total"] / ms["total"]
-    return {
-        "value": round(1.0 / per_target, 6),
-        "unit": "segment-proofs/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": (f"oracle proof of a 2^{log_n_sample}-row synthetic segment (same options) took {dt:.1f}s "
-                   f"with {threads} threads; scaled x{mt['total'] / ms['total']:.2f} by the Poseidon-permutation "
-                   f"work model to a 2^{log_n_target}-row segment"),
-        "sample_seconds": round(dt, 2),
-    }
+    out = {"unit": "segment-proofs/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+           "sample_seconds": round(dt, 2), "stage_seconds": stages}
+    if log_n == log_n_target:
+        out["value"] = round(1.0 / dt, 6)
+        out["sample"] = (f"one full oracle proof of the headline segment (2^{log_n} rows x {w} cols, blowup 16, q 64, "
+                         f"grind 16, partitions ({opts.num_partitions},{opts.hash_rate})) using {threads} threads "
+                         f"inside the proof; measured, not extrapolated")
+        out["proof_equals_gpu_proof"] = (proof == gpu_proof) if gpu_proof is not None else None
+    else:
+        ms, mt = perm_model(n), perm_model(1 << log_n_target)
+        out["value"] = round(1.0 / (dt * mt["total"] / ms["total"]), 6)
+        out["sample"] = (f"EXTRAPOLATED: oracle proof of a 2^{log_n}-row segment with {threads} threads took "
+                         f"{dt:.1f}s, scaled x{mt['total'] / ms['total']:.2f} by the permutation work model")
+    return out
 
 
+def valu_roofline(perms_per_s):
+    """Achieved permutations/s of the row hash against the ceiling its own instruction mix
+    implies at the measured per-class VALU rates (tools/valu_mix.py -> profiles/r02/valu_mix.json)."""
+    try:
+        mix = json.load(open(VALU_MIX))
+    except (OSError, ValueError):
+        return None
+    peak = mix["peak_perms_per_s"]
+    return {"bound": "valu-issue (instruction-mix ceiling)", "kernel": mix["kernel"],
+            "achieved": round(perms_per_s / 1e6, 1), "peak": round(peak / 1e6, 1), "unit": "M permutations/s",
+            "frac": round(perms_per_s / peak, 4),
+            "valu_per_perm_round_loop": mix["valu_per_perm_round_loop"],
+            "f128_mulmods_per_s": round(perms_per_s * MULMODS_PER_PERM),
+            "note": "peak = 32/27 wave-rounds per sum_c(count_c / rate_c) over the round loop's VALU classes, "
+                    "rates measured by tools/madbench.hip (profiles/r01/madbench.txt); the 12x12 MDS runs on "
+                    "v_mfma_i32_32x32x32_i8 and is not VALU work"}
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of the newest round."""
+    for r in ("r02", "r01"):
+        p = os.path.join(ROOT, "profiles", r, "pmc_traffic.json")
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if kernel in d:
+            return d[kernel]
+    return None
+
+
+# ------------------------------------------------------------------------ launcher
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """--gpus n without a torch.distributed.run environment: start n ranks of this script as
+    child processes (fresh interpreters; this process never initialises HIP), relay rank 0's
+    stdout, return non-zero if any rank fails."""
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    out0 = procs[0].stdout.read()
+    rcs = [p.wait() for p in procs]
+    if any(rcs):
+        log(f"bench: rank exit codes {rcs}")
+        return next(rc for rc in rcs if rc) if all(rc >= 0 for rc in rcs) else 1
+    sys.stdout.buffer.write(out0)
+    sys.stdout.flush()
+    return 0
+
+
+# ------------------------------------------------------------------------ workloads
 def c5_single(zkl_hip, device, log_n):
     """BASELINE configs[4] shape on one GPU: one synthetic 2^log_n-row segment (blowup 16,
     q 64, grind 16, partitions (16,16) at 2^20 rows), trace resident in HBM; on 8 GPUs each
@@ -122,57 +234,77 @@ def c5_single(zkl_hip, device, log_n):
     return ms, len(proof)
 
 
-def c3_pipeline(zkl_hip, device, log_n, n_segments, inflight, reps=1):
-    """BASELINE configs[2] shape: n_segments distinct 2^log_n-row segments proved on one GPU
-    with `inflight` contexts (one HIP stream each) in host threads, so one segment's
-    latency-bound tails (tree tops, FRI layers, transcript round trips) overlap another's
-    throughput phases.  Traces are resident in HBM before timing.  Returns segments/s."""
-    import threading
-    n = 1 << log_n
-    ctxs = [zkl_hip.Context(device) for _ in range(inflight)]
-    segs = []
-    for i in range(n_segments):
-        t, pi, w = zkl_hip.synth_vm_segment(0x5EED0001 + i, log_n)
-        c = ctxs[i % inflight]
-        d = c.alloc(w * n * 16)
-        c.upload(d, t, w * n * 16)
-        segs.append((c, d, pi, w, zkl_hip.proof_options(w, n)))
-    for k in range(inflight):  # warm each context (buffers, tables)
-        c, d, pi, w, o = segs[k]
-        c.prove_segment_device(d, w, n, pi, o)
-    best = None
-    for _ in range(reps):
-        def run(k):
-            for i in range(k, n_segments, inflight):
-                c, d, pi, w, o = segs[i]
-                c.prove_segment_device(d, w, n, pi, o)
-        th = [threading.Thread(target=run, args=(k,)) for k in range(inflight)]
-        for c in ctxs:
-            c.synchronize()
-        t0 = time.perf_counter()
+class Pipeline:
+    """A set of distinct segments resident in HBM, proved by `inflight` contexts (one HIP
+    stream each) in host threads, so one segment's latency-bound tails (tree tops, FRI
+    layers, transcript round trips) overlap another's throughput phases (BASELINE configs[2];
+    the reference's bounded segment pool, prove.rs:1018-1050)."""
+
+    def __init__(self, zkl_hip, device, log_n, seg_ids, inflight):
+        self.n = 1 << log_n
+        self.ctxs = [zkl_hip.Context(device) for _ in range(inflight)]
+        self.segs = []
+        for k, i in enumerate(seg_ids):
+            t, pi, w = zkl_hip.synth_vm_segment(SEED0 + i, log_n)
+            c = self.ctxs[k % inflight]
+            d = c.alloc(w * self.n * 16)
+            c.upload(d, t, w * self.n * 16)
+            self.segs.append([i, c, d, pi, w, zkl_hip.proof_options(w, self.n), None])
+        for k in range(min(inflight, len(self.segs))):  # warm each context (buffers, tables)
+            _, c, d, pi, w, o, _ = self.segs[k]
+            c.prove_segment_device(d, w, self.n, pi, o)
+
+    def run(self):
+        import threading
+        inflight = len(self.ctxs)
+
+        def work(k):
+            for s in self.segs[k::inflight]:
+                s[6] = s[1].prove_segment_device(s[2], s[4], self.n, s[3], s[5])
+
+        th = [threading.Thread(target=work, args=(k,)) for k in range(inflight)]
         for x in th:
             x.start()
         for x in th:
             x.join()
-        for c in ctxs:
+        for c in self.ctxs:
             c.synchronize()
-        dt = time.perf_counter() - t0
-        best = dt if best is None else min(best, dt)
-    for c, d, *_ in segs:
-        c.free(d)
-    for c in ctxs:
-        c.close()
-    return n_segments / best
+
+    def proofs(self):
+        return [(s[0], s[3], s[6]) for s in self.segs]
+
+    def close(self):
+        for s in self.segs:
+            s[1].free(s[2])
+        for c in self.ctxs:
+            c.close()
 
 
-def load_traffic(kernel):
-    """HBM bytes per launch from the committed PMC summary (profiles/r01/pmc_traffic.json)."""
-    p = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
-    try:
-        d = json.load(open(p))
-        return d.get(kernel)
-    except Exception:
+def step_info(zkl_hip, pi, index, total):
+    """zl1 step metadata of segment `index` of `total`; the synthetic boundary chain is
+    state_out(i) = state_in(i+1) = i+1 (what the aggregation checks)."""
+    info = zkl_hip.StepInfo()
+    info.suite_id[:] = bytes(pi.program_id)
+    info.lambda_bits, info.segment_index, info.segments_total = 128, index, total
+    info.state_in_hash[:] = index.to_bytes(32, "little")
+    info.state_out_hash[:] = (index + 1).to_bytes(32, "little")
+    return info
+
+
+def handoff(zkl_hip, dist, items, total):
+    """Aggregation hand-off: each rank wraps its proofs as zl1 steps (ZKLSTP1),
+    rank 0 gathers, orders and chain-checks them and forms the children root the aggregation
+    proof commits to (agg/child.rs:853-895)."""
+    t_h = time.perf_counter()
+    steps = dist.collect_step_proofs([zkl_hip.step_proof_encode(pi, step_info(zkl_hip, pi, i, total), proof)
+                                      for i, pi, proof in items])
+    if steps is None:
         return None
+    root = zkl_hip.children_root(bytes(steps[0]["program_id"]), [d["digest"] for d in steps],
+                                 [d["root_trace"] for d in steps])
+    return {"segments": len(steps), "step_bytes": sum(d["bytes"] for d in steps),
+            "ms": round((time.perf_counter() - t_h) * 1e3, 2), "children_root": root[:16].hex(),
+            "transport": "gloo (host bytes; the proofs already live in host memory)"}
 
 
 def main():
@@ -181,13 +313,30 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log-n", type=int, default=16)
-    ap.add_argument("--cpu-sample-log-n", type=int, default=14)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0: min(16, host CPUs))")
+    ap.add_argument("--cpu-sample-log-n", type=int, default=0,
+                    help="rows (log2) of the oracle proof timed for cpu_baseline (0: the headline size, measured)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0: OMP_NUM_THREADS or min(16, CPUs))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c3-segments", type=int, default=8, help="segments for the configs[2] pipeline line (0: skip)")
     ap.add_argument("--c3-inflight", type=str, default="1,2,4", help="contexts in flight to try for configs[2]")
+    ap.add_argument("--segments", type=int, default=-1,
+                    help="configs[3] shape: distinct segments sharded over the ranks (-1: 8 x N when N > 1, else 0)")
+    ap.add_argument("--inflight", type=int, default=4, help="contexts in flight per rank for --segments")
     ap.add_argument("--c5-log-n", type=int, default=20, help="rows (log2) of the configs[4] single-segment line (0: skip)")
+    ap.add_argument("--dry-run", action="store_true", help="launcher / rank plumbing only, no device work (CPU tests)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        log("bench: --gpus must be >= 1")
+        return 2
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus)
+
+    from zkl_hip import dist
+    rank, world, local_rank = dist.env()
+    if world != args.gpus:
+        log(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+            f"(torch.distributed.run --nproc-per-node {args.gpus}) or omit WORLD_SIZE to let bench.py start them")
+        return 2
 
     # Only the result line goes to stdout: native libraries (gloo prints "[Gloo] Rank ..."
     # from C++) write to fd 1, so fd 1 is pointed at stderr and the JSON line is written
@@ -195,22 +344,42 @@ def main():
     sys.stdout.flush()
     result_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+    dist.init()  # gloo control plane only (zkl_hip/dist.py)
+    n_seg = args.segments if args.segments >= 0 else (8 * world if world > 1 else 0)
 
-    from zkl_hip import dist
-    rank, world, local_rank = dist.init()  # gloo control plane only (zkl_hip/dist.py)
+    if args.dry_run:
+        dist.barrier()
+        t0 = time.perf_counter()
+        dist.barrier()
+        elapsed = dist.max_over_ranks(time.perf_counter() - t0)
+        mine = dist.segments_for_rank(n_seg, rank, world)
+        got = dist.gather_to_root({"rank": rank, "segments": mine})
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "dry_run": True,
+                              "elapsed_s": elapsed, "segments_by_rank": {g["rank"]: g["segments"] for g in got}}),
+                  file=result_out, flush=True)
+        dist.shutdown()
+        return 0
 
     import zkl_hip
-    # ZKL_BENCH_DEVICE pins every rank to one device (rehearsing N > 1 on a 1-GPU box)
-    device = int(os.environ.get("ZKL_BENCH_DEVICE", local_rank))
+    pinned = os.environ.get("ZKL_BENCH_DEVICE")
+    device = int(pinned) if pinned is not None else local_rank
+    n_dev = zkl_hip.device_count()
+    if device >= n_dev:
+        log(f"bench: rank {rank} needs device {device} but {n_dev} HIP device(s) are visible "
+            f"(set ZKL_BENCH_DEVICE to rehearse {world} ranks on fewer GPUs)")
+        return 3
     ctx = zkl_hip.Context(device)
     log_n = args.log_n
     n = 1 << log_n
-    trace, pi, W = zkl_hip.synth_vm_segment(0x5EED0001 + rank, log_n)
+    seed = SEED0 + rank
+    trace, pi, W = zkl_hip.synth_vm_segment(seed, log_n)
     opts = zkl_hip.proof_options(W, n)
     nbytes = W * n * 16
     d_trace = ctx.alloc(nbytes)
     ctx.upload(d_trace, trace, nbytes)
-    log(f"[rank {rank}] trace {W}x{n} resident in HBM; warmup {args.warmup}")
+    del trace
+    log(f"[rank {rank}] device {device}: trace {W}x{n} resident in HBM; warmup {args.warmup}")
 
     proof = None
     for _ in range(args.warmup):
@@ -232,38 +401,46 @@ def main():
     dist.barrier()
     elapsed = dist.max_over_ranks(time.perf_counter() - t0)
     host = ctx.host_times()
-    stages = {}
+    parity = dist.gather_to_root(parity_of(proof, seed, log_n))
+    stages, fam = {}, {}
     # Inside the timed region only the dominant family (the trace row hash) is bracketed by
     # HIP events (each bracket costs ~10 us of queue time); one extra untimed proof with
     # every family bracketed gives the per-family breakdown.
-    fam = {}
     if rank == 0:
         ctx.set_kernel_timing(2)
         ctx.prove_segment_device(d_trace, W, n, pi, opts)
         fam = ctx.kernel_times()
         stages = ctx.stage_times()
         ctx.set_kernel_timing(1)
-    # Aggregation hand-off (untimed): every rank wraps its last proof as zl1
-    # step `rank` of `world` (ZKLSTP1); rank 0 gathers, orders and chain-checks them and forms
-    # the children root the aggregation proof commits to (agg/child.rs:853-895).
-    t_h = time.perf_counter()
-    info = zkl_hip.StepInfo()
-    info.suite_id[:] = bytes(pi.program_id)
-    info.lambda_bits, info.segment_index, info.segments_total = 128, rank, world
-    info.state_in_hash[:] = rank.to_bytes(32, "little")  # synthetic chain: out(r) = in(r+1)
-    info.state_out_hash[:] = (rank + 1).to_bytes(32, "little")
-    steps = dist.collect_step_proofs([zkl_hip.step_proof_encode(pi, info, proof)])
-    handoff = None
-    if steps is not None:
-        root = zkl_hip.children_root(bytes(pi.program_id), [d["digest"] for d in steps],
-                                     [d["root_trace"] for d in steps])
-        handoff = {"segments": len(steps), "step_bytes": sum(d["bytes"] for d in steps),
-                   "ms": round((time.perf_counter() - t_h) * 1e3, 2), "children_root": root[:16].hex(),
-                   "transport": "gloo (host bytes; the proofs already live in host memory)"}
+    ctx.free(d_trace)
+    ctx.close()
+    hand = handoff(zkl_hip, dist, [(rank, pi, proof)], world)
+
+    # configs[3] shape: S distinct segments sharded over the ranks, pipelined per rank
+    c4 = None
+    if n_seg > 0:
+        mine = dist.segments_for_rank(n_seg, rank, world)
+        pl = Pipeline(zkl_hip, device, log_n, mine, max(1, min(args.inflight, len(mine))))
+        dist.barrier()
+        t1 = time.perf_counter()
+        pl.run()
+        dist.barrier()
+        el4 = dist.max_over_ranks(time.perf_counter() - t1)
+        items = pl.proofs()
+        par4 = dist.gather_to_root([parity_of(p, SEED0 + i, log_n)["golden"] for i, _, p in items])
+        pl.close()
+        h4 = handoff(zkl_hip, dist, items, n_seg)
+        if rank == 0:
+            flat = [g for r in par4 for g in r]
+            c4 = {"config": f"BASELINE configs[3] shape: {n_seg} distinct synthetic 2^{log_n}-row segments sharded "
+                            f"over {world} rank(s), {args.inflight} contexts in flight per rank, then the step-proof "
+                            "gather and children root on rank 0",
+                  "value": round(n_seg / el4, 4), "unit": "segment-proofs/s", "seconds": round(el4, 3),
+                  "golden_matches": flat.count("match"), "golden_mismatches": flat.count("MISMATCH"),
+                  "handoff": h4}
 
     if rank == 0:
         value = world * args.steps / elapsed
-        # dominant kernel family (from the breakdown proof) and its roofline (timed region)
         dom = max(fam.items(), key=lambda kv: kv[1][0])[0] if fam else "trace_hash_rows"
         ms_tot, launches = kacc["trace_hash_rows"]
         per_launch_ms = ms_tot / max(launches, 1)
@@ -276,8 +453,7 @@ def main():
         perms_per_s = perms_per_launch / (per_launch_ms * 1e-3)
         engine = "lane" if os.environ.get("ZKL_HASH_ENGINE") == "lane" else "mfma"
         kname = ROW_KERNEL[engine]
-        valu_g = perms_per_s * VALU_INSTR_PER_PERM[engine] / 1e9
-        traffic = load_traffic(kname)
+        mism = sum(p["golden"] == "MISMATCH" for p in parity)
         out = {
             "metric": METRIC,
             "value": round(value, 4),
@@ -296,8 +472,13 @@ def main():
                             f"grind 16, partitions ({opts.num_partitions},{opts.hash_rate}); trace resident in HBM",
                 "rows": n, "width": W, "blowup": 16, "queries": 64, "grind": 16,
                 "segments_per_gpu_per_step": 1, "parallelism": f"segments x{world} (one rank per GPU)",
+                "devices": "all ranks pinned to device " + pinned if pinned is not None else "one per rank",
                 "proof_bytes": len(proof),
             },
+            "parity": {"status": "ok" if mism == 0 and all(p["golden"] == "match" for p in parity)
+                       else ("MISMATCH" if mism else "no golden for some ranks"),
+                       "reference": "CPU oracle proof bytes (tests/golden/proof_2p16.json)",
+                       "ranks": parity},
             "roofline": {
                 "bound": "hbm",
                 "kernel": f"{kname} (trace LDE row hashing, 4 partitions + merge_many)",
@@ -305,40 +486,42 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": traffic,
+                "traffic": load_traffic(kname),
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": round(per_launch_ms, 3),
                 "note": "VALU-issue bound (integer Poseidon); see roofline_valu",
             },
-            "roofline_valu": {
-                "bound": "valu-issue",
-                "kernel": kname,
-                "achieved": round(valu_g, 1),
-                "peak": VALU_ISSUE_PEAK_G,
-                "unit": "G VALU wave-instructions/s",
-                "frac": round(valu_g / VALU_ISSUE_PEAK_G, 4),
-                "perms_per_launch": perms_per_launch,
-                "perms_per_s": round(perms_per_s),
-                "f128_mulmods_per_s": round(perms_per_s * MULMODS_PER_PERM),
-                "note": "VALU wave-instructions per permutation from SQ_INSTS_VALU (profiles/r01/pmc_sq_pm.json); "
-                        "the 12x12 MDS runs on the matrix cores (MFMA busy ~21% of cycles)",
-            },
+            "roofline_valu": valu_roofline(perms_per_s),
             "dominant_kernel_family": dom,
             "kernel_ms_per_family_untimed_step": {k: round(v[0], 3) for k, v in fam.items()},
+            "kernel_launches_per_family_untimed_step": {k: v[1] for k, v in fam.items()},
             "stage_ms_untimed_step": {k: round(v, 3) for k, v in stages.items()},
             "host_ms_last_step": {k: round(v, 3) for k, v in host.items()},
             "call_ms_each_step": [round(v, 2) for v in step_ms],
-            "step_handoff": handoff,
+            "step_handoff": hand,
         }
+        if c4 is not None:
+            out["c4_sharded"] = c4
         if world == 1 and args.c3_segments > 0:
             c3 = {}
             for k in [int(x) for x in args.c3_inflight.split(",") if x]:
-                c3[str(k)] = round(c3_pipeline(zkl_hip, device, log_n, args.c3_segments, k), 4)
+                pl = Pipeline(zkl_hip, device, log_n, list(range(args.c3_segments)), k)
+                best = None
+                for _ in range(2):
+                    t1 = time.perf_counter()
+                    pl.run()
+                    dt = time.perf_counter() - t1
+                    best = dt if best is None else min(best, dt)
+                if k == max(int(x) for x in args.c3_inflight.split(",") if x):
+                    g = [parity_of(p, SEED0 + i, log_n)["golden"] for i, _, p in pl.proofs()]
+                    c3_par = {"golden_matches": g.count("match"), "golden_mismatches": g.count("MISMATCH")}
+                pl.close()
+                c3[str(k)] = round(args.c3_segments / best, 4)
             kbest = max(c3, key=lambda k: c3[k])
             out["c3_in_gpu_pipeline"] = {
                 "config": f"BASELINE configs[2] shape: {args.c3_segments} distinct synthetic 2^{log_n}-row segments on 1 GPU",
                 "segment_proofs_per_s_by_inflight": c3, "best_inflight": int(kbest), "value": c3[kbest],
-                "unit": "segment-proofs/s"}
+                "unit": "segment-proofs/s", "parity": c3_par}
         if world == 1 and args.c5_log_n > 0:
             try:
                 ms5, pb5 = c5_single(zkl_hip, device, args.c5_log_n)
@@ -351,15 +534,16 @@ def main():
                 out["c5_single_segment"] = {"error": str(e)}
         if world == 1 and not args.no_cpu_baseline:
             try:
-                th = args.cpu_threads or min(16, os.cpu_count() or 1)
-                out["cpu_baseline"] = cpu_baseline(args.cpu_sample_log_n, log_n, th)
+                out["cpu_baseline"] = cpu_baseline(args.cpu_sample_log_n or log_n, cpu_threads(args.cpu_threads),
+                                                   proof, log_n)
+                if out["cpu_baseline"].get("proof_equals_gpu_proof") is False:
+                    out["parity"]["status"] = "MISMATCH"
             except Exception as e:  # reported, never fatal for the GPU number
                 out["cpu_baseline"] = {"value": None, "error": str(e)}
         print(json.dumps(out), file=result_out, flush=True)
-    ctx.free(d_trace)
-    ctx.close()
     dist.shutdown()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -141,6 +141,16 @@ int zkl_hip_prove_segment_device(zkl_ctx* ctx, const void* d_trace, uint32_t wid
                                  const zkl_air_public_inputs* pi, const zkl_proof_options* opts,
                                  uint8_t** proof_out, size_t* proof_len);
 
+/* The request checks zkl_hip_prove_segment* run before any device work, without a device:
+ * ProofOptions / PartitionOptions bounds (num_queries 1..255, blowup a power of two >= 2 and
+ * >= the AIR's constraint-evaluation blowup, num_partitions 1..16, hash_rate 1..256, FRI
+ * folding 2, remainder degree 2^k - 1), the supported options (FieldExtension::None,
+ * BatchingMethod::Linear), the trace shape (n_rows a power of two >= 32, width = the segment
+ * layout's width) and the public-input shape (n_main_slots <= ZKL_MAX_MAIN_SLOTS, assertion
+ * count = AirContext::num_assertions).  ZKL_OK or ZKL_E_INVALID + zkl_hip_last_error(NULL). */
+int zkl_hip_check_request(uint32_t width, uint32_t n_rows, const zkl_air_public_inputs* pi,
+                          const zkl_proof_options* opts);
+
 /* Host-side wall times (ms) of the last proof on ctx: [0] host setup before the first
  * kernel (AIR instance, assertions, uploads), [1] host time between the first and last
  * stage marks not covered by device work, [2] the whole call.  Returns number written. */
@@ -191,6 +201,16 @@ int zkl_hip_poseidon_permute(zkl_ctx* ctx, void* d_states, uint32_t n_states, in
  * pm_min_items states (default 16384) on the matrix-core permutation, engine 0 keeps every
  * level on lane groups.  Both give identical digests; this only moves time. */
 int zkl_hip_set_hash_policy(int engine, uint32_t pm_min_items);
+/* Process-wide row-digest rule for partitioned rows that form a single chunk (partition
+ * size > row width: the 7-column composition rows from 2^14 trace rows up, any matrix
+ * narrower than its partition size).  0 (default): winterfell 0.13.1
+ * RowMatrix::commit_to_rows — merge_many over the chunk digests whenever partition_size !=
+ * num_cols, even of one digest; 1: the reference's own re-implementation
+ * hash_row_poseidon (agg/child.rs:1025-1045), which returns a single chunk digest as is.
+ * Rows of several chunks and unpartitioned rows hash identically under both (DESIGN.md
+ * §3.1).  zkl_hip_row_digest_rule() returns the rule in force. */
+int zkl_hip_set_row_digest_rule(int rule);
+int zkl_hip_row_digest_rule(void);
 /* Process-wide NTT form for evaluation (DIT) passes: 1 (default) lazily reduced 26-bit limbs
  * inside a pass, 0 the canonical-form kernel.  Identical results; for parity tests / A-B. */
 int zkl_hip_set_ntt_mode(int lazy);

@@ -88,3 +88,10 @@ int orc_api_check_trace(const zkl_f128 *t, uint32_t w, size_t n, const zkl_air_p
   air_free(&a);
   return bad ? 1 : 0;
 }
+/* digest of one row (ncols elements) partitioned into chunks of psize under the current rule */
+void orc_api_row_digest(const uint8_t *row, size_t ncols, size_t psize, uint8_t *o) {
+  fe *v = (fe *)malloc((ncols ? ncols : 1) * sizeof(fe));
+  for (size_t i = 0; i < ncols; i++) v[i] = rd(row + 16 * i);
+  wr(orc_row_digest(v, ncols, psize), o);
+  free(v);
+}

@@ -126,6 +126,11 @@ int orc_prove_segment(const zkl_f128 *trace, uint32_t width, uint32_t n,
 int orc_verify_segment(const uint8_t *proof, size_t len, const zkl_air_public_inputs *pi,
                        const zkl_proof_options *opts, char *err, size_t errlen);
 void orc_free(void *p);
+/* row digest of a (partitioned) row; rule 0 winterfell commit_to_rows, rule 1 agg/child.rs
+ * hash_row_poseidon (differ only for one-chunk rows, prover.c) */
+fe orc_row_digest(const fe *row, size_t ncols, size_t psize);
+void orc_set_row_digest_rule(int rule);
+int orc_row_digest_rule(void);
 
 /* ---------------- zl1 step proof (proof/step.rs, format.rs, digest.rs) ---------------- */
 int orc_step_encode(const zkl_air_public_inputs *pi, const zkl_step_info *s, const uint8_t *inner, size_t inner_len,

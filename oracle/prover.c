@@ -143,20 +143,34 @@ static size_t partition_size(uint32_t np, uint32_t rate, size_t ncols) {
   size_t a = (ncols + np - 1) / np;
   return a > rate ? a : rate;
 }
-static fe hash_row(const fe *row, size_t ncols, size_t psize) {
+/* Row digest of a partitioned row (PartitionOptions).  Two rules differ only for
+ * a row whose partition size exceeds its width, i.e. one chunk (composition rows at
+ * n >= 2^14; any matrix narrower than its partition size):
+ *   rule 0 (default) winterfell 0.13.1 RowMatrix::commit_to_rows [WF-recall]: hash_elements
+ *          when partition_size == num_cols, otherwise merge_many over the chunk digests,
+ *          even of a single digest;
+ *   rule 1 the reference's own restatement agg/child.rs:1025-1045 (hash_row_poseidon):
+ *          a single chunk digest is returned as is.
+ * DESIGN.md §3.1 records why rule 0 is the default. */
+int g_orc_row_digest_rule = 0;
+void orc_set_row_digest_rule(int r) { g_orc_row_digest_rule = r ? 1 : 0; }
+int orc_row_digest_rule(void) { return g_orc_row_digest_rule; }
+
+fe orc_row_digest(const fe *row, size_t ncols, size_t psize) {
   if (psize == ncols) return ph_hash_elements(row, ncols);
-  fe d[64];
+  fe d[256];
   size_t np = 0;
   for (size_t s = 0; s < ncols; s += psize) {
     size_t l = ncols - s < psize ? ncols - s : psize;
     d[np++] = ph_hash_elements(row + s, l);
   }
+  if (np == 1 && g_orc_row_digest_rule == 1) return d[0];
   return ph_merge_many(d, np);
 }
 static void hash_rows(const fe *rows, size_t nrows, size_t ncols, uint32_t np, uint32_t rate, fe *out) {
   size_t ps = partition_size(np, rate, ncols);
 #pragma omp parallel for num_threads(g_orc_threads) schedule(dynamic, 64)
-  for (size_t r = 0; r < nrows; r++) out[r] = hash_row(rows + r * ncols, ncols, ps);
+  for (size_t r = 0; r < nrows; r++) out[r] = orc_row_digest(rows + r * ncols, ncols, ps);
 }
 
 /* ------------------------------------------------------------------ proof */

@@ -165,16 +165,6 @@ static size_t part_size(uint32_t np, uint32_t rate, size_t ncols) {
   size_t a = (ncols + np - 1) / np;
   return a > rate ? a : rate;
 }
-static fe row_digest(const fe *row, size_t ncols, size_t psize) {
-  if (psize == ncols) return ph_hash_elements(row, ncols);
-  fe d[256];
-  size_t np = 0;
-  for (size_t s = 0; s < ncols; s += psize) {
-    size_t l = ncols - s < psize ? ncols - s : psize;
-    d[np++] = ph_hash_elements(row + s, l);
-  }
-  return ph_merge_many(d, np);
-}
 static unsigned lg2(size_t n) { unsigned k = 0; while (((size_t)1 << k) < n) k++; return k; }
 
 #define FAIL(msg)                                     \
@@ -331,11 +321,11 @@ int orc_verify_segment(const uint8_t *proof, size_t len, const zkl_air_public_in
   {
     fe root;
     size_t ps = part_size(opts->num_partitions, opts->hash_rate, W);
-    for (size_t k = 0; k < nq; k++) leafd[k] = row_digest(tvals + k * W, W, ps);
+    for (size_t k = 0; k < nq; k++) leafd[k] = orc_row_digest(tvals + k * W, W, ps);
     if (batch_root(&tq_p, N, pos, leafd, nq, &root) || root != troot || tq_p.off != tq_p.len)
       FAIL("trace Merkle opening does not reproduce the trace commitment");
     ps = part_size(opts->num_partitions, opts->hash_rate, (size_t)C);
-    for (size_t k = 0; k < nq; k++) leafd[k] = row_digest(cvals + k * C, (size_t)C, ps);
+    for (size_t k = 0; k < nq; k++) leafd[k] = orc_row_digest(cvals + k * C, (size_t)C, ps);
     if (batch_root(&cq_p, N, pos, leafd, nq, &root) || root != croot || cq_p.off != cq_p.len)
       FAIL("constraint Merkle opening does not reproduce the constraint commitment");
   }

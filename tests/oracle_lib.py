@@ -205,6 +205,26 @@ def check_trace(trace, pi, width, n):
     return rc, br.value, bi.value
 
 
+def set_row_digest_rule(rule):
+    """0: winterfell commit_to_rows (default); 1: agg/child.rs:1025-1045 hash_row_poseidon."""
+    lib().orc_set_row_digest_rule(C.c_int(rule))
+
+
+def row_digest_rule():
+    return lib().orc_row_digest_rule()
+
+
+def row_digest(row, psize):
+    o = _buf(16)
+    lib().orc_api_row_digest(b"".join(fe_bytes(x) for x in row), C.c_size_t(len(row)), C.c_size_t(psize), o)
+    return fe_from(o)
+
+
+def partition_size(np_, rate, ncols):
+    """PartitionOptions::partition_size for the base field (ExtensionDegree 1)."""
+    return ncols if np_ <= 1 else max(-(-ncols // np_), rate)
+
+
 def set_threads(t):
     lib().orc_set_threads(C.c_int(t))
 

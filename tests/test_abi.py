@@ -67,3 +67,64 @@ def test_init_without_gpu_fails_cleanly():
         pytest.skip("GPU present")
     with pytest.raises(zkl_hip.ZklError):
         zkl_hip.Context(0)
+
+
+def _req(log_n=6, **kw):
+    import zkl_hip
+    t, pi, w = zkl_hip.synth_vm_segment(0x5EED0300, max(log_n, 5))
+    opts = zkl_hip.proof_options(w, 1 << max(log_n, 5), queries=8, grind=0)
+    for k, v in kw.items():
+        if hasattr(opts, k):
+            setattr(opts, k, v)
+    if "n_main_slots" in kw:
+        pi.n_main_slots = kw["n_main_slots"]
+    return w - kw.get("width_delta", 0), 1 << log_n, pi, opts
+
+
+def test_check_request_accepts_valid():
+    import zkl_hip
+    for log_n in (5, 8, 14, 16):
+        w, n, pi, opts = _req(log_n)
+        zkl_hip.check_request(w, n, pi, opts)
+
+
+@pytest.mark.parametrize("change,msg", [
+    (dict(log_n=4), "power of two >= 32"),
+    (dict(blowup_factor=4), "blowup factor below"),
+    (dict(blowup_factor=12), "power of two"),
+    (dict(blowup_factor=1), "power of two"),
+    (dict(num_queries=0), "num_queries"),
+    (dict(num_queries=256), "num_queries"),
+    (dict(field_extension=2), "FieldExtension::None"),
+    (dict(fri_folding_factor=4), "folding factor"),
+    (dict(fri_remainder_max_degree=2), "fri_remainder_max_degree"),
+    (dict(batching_constraints=1), "Linear"),
+    (dict(batching_deep=1), "Linear"),
+    (dict(num_partitions=0), "num_partitions"),
+    (dict(num_partitions=17), "num_partitions"),
+    (dict(num_partitions=64), "num_partitions"),
+    (dict(hash_rate=0), "hash_rate"),
+    (dict(hash_rate=257), "hash_rate"),
+    (dict(n_main_slots=9), "ZKL_MAX_MAIN_SLOTS"),
+    (dict(n_main_slots=1000), "ZKL_MAX_MAIN_SLOTS"),
+    (dict(width_delta=1), "width"),
+])
+def test_check_request_rejections(change, msg):
+    """Each request the prover refuses is refused on the host, before any device work, with
+    ZKL_E_INVALID and a message (n_main_slots read past main_slots, unchecked
+    num_partitions / hash_rate)."""
+    import zkl_hip
+    w, n, pi, opts = _req(**change)
+    with pytest.raises(zkl_hip.ZklError, match=msg) as ei:
+        zkl_hip.check_request(w, n, pi, opts)
+    assert ei.value.code == -1
+
+
+def test_row_digest_rule_switch():
+    import zkl_hip
+    lib = zkl_hip.load_library()
+    assert lib.zkl_hip_row_digest_rule() == 0
+    with zkl_hip.row_digest_rule(1):
+        assert lib.zkl_hip_row_digest_rule() == 1
+    assert lib.zkl_hip_row_digest_rule() == 0
+    assert lib.zkl_hip_set_row_digest_rule(2) == -1

@@ -536,3 +536,127 @@ def test_full_size_proof_independent_of_kernel_forms(gpu_ctx):
         lib.zkl_hip_set_ntt_mode(1)
     ref = proofs["default"]
     assert all(p == ref for p in proofs.values()), [k for k, p in proofs.items() if p != ref]
+
+
+# ---------------------------------------------------------------------------------------
+# Headline configuration (BASELINE configs[1]: 2^16 rows, blowup 16, q 64, grind 16,
+# partitions (4, 16)): proof bytes against the CPU oracle's, via the committed goldens
+# (tests/golden/make_proof_goldens.py) and one direct oracle proof.  These cover the
+# 4-partition trace row digest (4 x 51 columns + merge_many) and the one-chunk composition
+# row digest (7 columns < partition size 16) at proof level.
+# ---------------------------------------------------------------------------------------
+def _goldens():
+    import json
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "proof_2p16.json")
+    return json.load(open(p))
+
+
+@pytest.mark.parametrize("name", sorted(_goldens()))
+def test_headline_proof_matches_golden(gpu_ctx, name):
+    import zkl_hip
+    g = _goldens()[name]
+    n = 1 << g["log_n"]
+    t, pi, w = zkl_hip.synth_vm_segment(g["seed"], g["log_n"], g["flags"])
+    assert w == g["width"]
+    opts = zkl_hip.proof_options(w, n)
+    assert {f: getattr(opts, f) for f, _ in opts._fields_} == g["options"]
+    assert (opts.num_partitions, opts.hash_rate) == (4, 16)
+    got = gpu_ctx.prove_segment(t, w, n, pi, opts)
+    assert len(got) == g["len"]
+    assert hashlib.sha256(got).hexdigest() == g["sha256"]
+
+
+def test_headline_proof_equals_oracle_proof(oracle, gpu_ctx):
+    """One direct comparison at the headline configuration (no golden in between): the oracle
+    proves the same 2^16-row segment on the host (~40 s on 16 threads)."""
+    import os
+    import zkl_hip
+    n = 1 << 16
+    t, pi, w = zkl_hip.synth_vm_segment(0x5EED0001, 16)
+    opts = zkl_hip.proof_options(w, n)
+    got = gpu_ctx.prove_segment(t, w, n, pi, opts)
+    oracle.set_threads(int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ot, opi, _ = oracle.synth_segment(0x5EED0001, 16)
+    want = oracle.prove(ot, w, n, opi, _gpu_opts(oracle, opts))
+    oracle.set_threads(1)
+    assert got == want
+
+
+def test_c3_pipeline_bytes_match_sequential_and_goldens(gpu_ctx):
+    """configs[2] shape: 8 distinct 2^16-row segments proved by 4 contexts in flight on one
+    device (the bench's in-GPU pipeline) give, per segment, the same bytes as one context
+    proving them in turn, and those equal the oracle goldens."""
+    import threading
+    import zkl_hip
+    gold = {g["seed"]: g for g in _goldens().values() if g["flags"] == 0}
+    n = 1 << 16
+    segs = []
+    for i in range(8):
+        t, pi, w = zkl_hip.synth_vm_segment(0x5EED0001 + i, 16)
+        segs.append((t, pi, w, zkl_hip.proof_options(w, n)))
+    seq = [gpu_ctx.prove_segment(t, w, n, pi, o) for t, pi, w, o in segs]
+    ctxs = [zkl_hip.Context(0) for _ in range(4)]
+    dev = []
+    for k, (t, pi, w, o) in enumerate(segs):
+        c = ctxs[k % 4]
+        d = c.alloc(w * n * 16)
+        c.upload(d, t, w * n * 16)
+        dev.append(d)
+    got = [None] * 8
+
+    def run(k):
+        for i in range(k, 8, 4):
+            t, pi, w, o = segs[i]
+            got[i] = ctxs[k].prove_segment_device(dev[i], w, n, pi, o)
+
+    try:
+        th = [threading.Thread(target=run, args=(k,)) for k in range(4)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+    finally:
+        for k, d in enumerate(dev):
+            ctxs[k % 4].free(d)
+        for c in ctxs:
+            c.close()
+    assert got == seq
+    for i, p in enumerate(seq):
+        g = gold[0x5EED0001 + i]
+        assert len(p) == g["len"] and hashlib.sha256(p).hexdigest() == g["sha256"], f"segment {i}"
+
+
+@pytest.mark.parametrize("rule", [0, 1])
+def test_row_digest_rule_proofs_match_oracle(oracle, gpu_ctx, rule):
+    """Both one-chunk row-digest rules on the GPU equal the oracle under the
+    same rule, on a segment with partitions (2, 16): the trace rows form two chunks, the
+    composition rows one (the rows the rules disagree on)."""
+    import zkl_hip
+    n = 1 << 8
+    t, pi, w = zkl_hip.synth_vm_segment(0x5EED0A08, 8)
+    opts = zkl_hip.proof_options(w, n, queries=24, grind=4)
+    opts.num_partitions = 2
+    with zkl_hip.row_digest_rule(rule):
+        got = gpu_ctx.prove_segment(t, w, n, pi, opts)
+    ot, opi, _ = oracle.synth_segment(0x5EED0A08, 8)
+    oracle.set_row_digest_rule(rule)
+    try:
+        want = oracle.prove(ot, w, n, opi, _gpu_opts(oracle, opts))
+        assert oracle.verify(got, opi, _gpu_opts(oracle, opts))[0] == 0
+    finally:
+        oracle.set_row_digest_rule(0)
+    assert got == want
+
+
+@pytest.mark.parametrize("field,value,msg", [
+    ("num_partitions", 17, "num_partitions"), ("num_partitions", 0, "num_partitions"),
+    ("hash_rate", 300, "hash_rate"), ("fri_remainder_max_degree", 2, "fri_remainder_max_degree"),
+])
+def test_invalid_partition_options_rejected(gpu_ctx, field, value, msg):
+    import zkl_hip
+    t, pi, w = zkl_hip.synth_vm_segment(0x5EED0300, 6)
+    opts = zkl_hip.proof_options(w, 64, queries=8, grind=0)
+    setattr(opts, field, value)
+    with pytest.raises(zkl_hip.ZklError, match=msg):
+        gpu_ctx.prove_segment(t, w, 64, pi, opts)

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <map>
+#include <stdexcept>
 
 #include "host_hash.h"
 
@@ -167,6 +168,7 @@ std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n,
   // ---- assertions (ScheduleAir, VM PI, RomAir), dedup by (col, step), Winterfell order
   std::vector<Assertion> raw;
   size_t last = n - 1, lvls = n / STEPS;
+  if (pi.n_main_slots > ZKL_MAX_MAIN_SLOTS) return "n_main_slots exceeds ZKL_MAX_MAIN_SLOTS";
   fe pc_init = fe_from(pi.pc_init);
   for (size_t l = 0; l < lvls; l++) {
     uint32_t b = (uint32_t)(l * STEPS), rm = b, rf = b + 28;
@@ -233,6 +235,7 @@ std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n,
 }
 
 std::vector<fe> pi_elements(const zkl_air_public_inputs& pi) {
+  if (pi.n_main_slots > ZKL_MAX_MAIN_SLOTS) throw std::invalid_argument("n_main_slots exceeds ZKL_MAX_MAIN_SLOTS");
   std::vector<fe> out;
   out.push_back(fe{pi.feature_mask, 0});
   out.push_back(be_from_le16(pi.program_commitment));

@@ -2,10 +2,27 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <stdexcept>
+#include <string>
 #include "air_host.h"
 #include "field.h"
 
 namespace zkl {
+
+// HIP runtime failure (mapped to ZKL_E_DEVICE at the C ABI, with the failing call or kernel)
+struct DeviceError : std::runtime_error { using std::runtime_error::runtime_error; };
+#define ZKL_HIPCHECK(x)                                                                       \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess) throw ::zkl::DeviceError(std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+// after a group of kernel launches: a failed launch (bad configuration, resources) surfaces
+// here with the group's name instead of at some later synchronisation
+inline void check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw DeviceError(std::string("kernel launch failed (") + what + "): " + hipGetErrorString(e));
+}
 
 struct HasherConsts {  // PoseidonHasher suite [0;32] + folded domain labels
   fe mds[144];
@@ -30,6 +47,9 @@ void upload_pm_tables(const HasherConsts& h, hipStream_t s);
 // 1 = matrix-core permutation on throughput-bound levels (default), 0 = lane groups only
 int hash_engine();
 void set_hash_policy(int engine, size_t min_items);
+// one-chunk row digest rule (launch_hash_rows): 0 winterfell commit_to_rows, 1 agg/child.rs
+void set_row_digest_rule(int rule);
+int row_digest_rule();
 // DIT passes on lazily reduced limbs (default) or the canonical kernel
 void set_ntt_lazy(bool on);
 // n Poseidon permutations of 12-element canonical states in place (engine as above)

@@ -21,20 +21,22 @@ namespace zkl {
 
 
 void upload_air_consts(ProofConsts* dK, const AirDevice& a, hipStream_t s) {
-  (void)hipMemcpyAsync(&dK->air, &a, sizeof a, hipMemcpyHostToDevice, s);
+  ZKL_HIPCHECK(hipMemcpyAsync(&dK->air, &a, sizeof a, hipMemcpyHostToDevice, s));
 }
 void upload_alphas_from_device(ProofConsts* dK, const fe* d, int n, hipStream_t s) {
-  (void)hipMemcpyAsync(dK->alpha, d, sizeof(fe) * n, hipMemcpyDeviceToDevice, s);
+  if (n > 1024) throw std::invalid_argument("more than 1024 transition constraints");
+  ZKL_HIPCHECK(hipMemcpyAsync(dK->alpha, d, sizeof(fe) * n, hipMemcpyDeviceToDevice, s));
 }
 static void limbs26(fe a, uint32_t l[5]);
 void upload_deep_coeffs(ProofConsts* dK, const fe* h, int n, hipStream_t s) {
-  (void)hipMemcpyAsync(dK->deep, h, sizeof(fe) * n, hipMemcpyHostToDevice, s);
+  if (n > 512) throw std::invalid_argument("more than 512 DEEP coefficients");
+  ZKL_HIPCHECK(hipMemcpyAsync(dK->deep, h, sizeof(fe) * n, hipMemcpyHostToDevice, s));
   static thread_local std::vector<uint32_t> m;
   m.assign((size_t)n * 5, 0);
   const fe R = fe_pow64(fe{2, 0}, 156);
   for (int i = 0; i < n; i++) limbs26(fe_mul(h[i], R), &m[(size_t)i * 5]);
-  (void)hipMemcpyAsync(dK->deep_m, m.data(), m.size() * 4, hipMemcpyHostToDevice, s);
-  (void)hipStreamSynchronize(s);  // m is reused by the next proof on this thread
+  ZKL_HIPCHECK(hipMemcpyAsync(dK->deep_m, m.data(), m.size() * 4, hipMemcpyHostToDevice, s));
+  ZKL_HIPCHECK(hipStreamSynchronize(s));  // m is reused by the next proof on this thread
 }
 
 // =====================================================================================
@@ -173,7 +175,7 @@ HasherMont make_hasher_mont(const HasherConsts& h) {
 }
 
 void upload_hasher_mont(const HasherMont& m, hipStream_t s) {
-  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(c_hm), &m, sizeof m, 0, hipMemcpyHostToDevice, s);
+  ZKL_HIPCHECK(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_hm), &m, sizeof m, 0, hipMemcpyHostToDevice, s));
 }
 
 // ---- lane-group permutation ------------------------------------------------------------
@@ -435,12 +437,11 @@ static inline unsigned pg_blocks(size_t items) {
 // TAG only separates the trace (0) and composition (1) commitments in profiles
 template <int TAG>
 __global__ PG_KERNEL void hash_rows_kernel(const fe* __restrict__ M, uint32_t ncols, size_t nrows,
-                                                        uint32_t psize, fe* __restrict__ out) {
+                                                        uint32_t psize, uint32_t merge, fe* __restrict__ out) {
   PG_SETUP();
   const bool live = P.g < PG_PER_WAVE && item < nrows;
   const size_t row = live ? item : 0;
   const uint32_t np = (ncols + psize - 1) / psize;
-  const bool merge = psize != ncols;  // partitioned rows end in merge_many, even of one digest
   fe keep0 = fe_zero(), keep1 = fe_zero(), d = fe_zero();
   for (uint32_t p = 0; p < np; p++) {
     const uint32_t c0 = p * psize;
@@ -490,6 +491,13 @@ __global__ PG_KERNEL void grind_kernel(fe seed, uint64_t base, uint32_t count, u
   }
 }
 
+// Row-digest rule for one-chunk partitioned rows (partition size > width): 0 = winterfell
+// commit_to_rows (merge_many of the single chunk digest), 1 = agg/child.rs:1025-1045
+// (the chunk digest itself).  DESIGN.md §3.1; the oracle has the same switch.
+static std::atomic<int> g_row_rule{0};
+void set_row_digest_rule(int r) { g_row_rule.store(r ? 1 : 0); }
+int row_digest_rule() { return g_row_rule.load(); }
+
 void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np, uint32_t rate, fe* d_tmp, fe* d_out,
                       hipStream_t s, int tag) {
   (void)d_tmp;
@@ -499,17 +507,19 @@ void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np
     if (psize < rate) psize = rate;  // PartitionOptions::partition_size, ExtensionDegree 1
   }
   const uint32_t np_eff = (ncols + psize - 1) / psize;
+  // partitioned rows end in merge_many (rule 0: even of one digest)
+  const uint32_t merge = row_digest_rule() == 0 ? (psize != ncols) : (np_eff > 1);
   if (hash_engine() == 1 && nrows >= pm_min_items() && np_eff <= (uint32_t)PM_MAX_PARTS) {
     if (tag == 1)
-      PM_GO(hash_rows_pm_kernel<1>, nrows, true, s)(d_mat, ncols, nrows, psize, d_out);
+      PM_GO(hash_rows_pm_kernel<1>, nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out);
     else
-      PM_GO(hash_rows_pm_kernel<0>, nrows, true, s)(d_mat, ncols, nrows, psize, d_out);
+      PM_GO(hash_rows_pm_kernel<0>, nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out);
     return;
   }
   if (tag == 1)
-    hash_rows_kernel<1><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, d_out);
+    hash_rows_kernel<1><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, merge, d_out);
   else
-    hash_rows_kernel<0><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, d_out);
+    hash_rows_kernel<0><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, merge, d_out);
 }
 
 __global__ __launch_bounds__(256) void merkle_level_wide_kernel(fe* nodes, size_t lvl) {
@@ -677,9 +687,9 @@ void build_mont_table(const fe* w, size_t N, void* d_buf, hipStream_t s) {
       l1[H + j] = l[4];
     }
   }
-  (void)hipMemcpyAsync(d_buf, l4.data(), N * 16, hipMemcpyHostToDevice, s);
-  (void)hipMemcpyAsync((char*)d_buf + N * 16, l1.data(), N * 4, hipMemcpyHostToDevice, s);
-  (void)hipStreamSynchronize(s);
+  ZKL_HIPCHECK(hipMemcpyAsync(d_buf, l4.data(), N * 16, hipMemcpyHostToDevice, s));
+  ZKL_HIPCHECK(hipMemcpyAsync((char*)d_buf + N * 16, l1.data(), N * 4, hipMemcpyHostToDevice, s));
+  ZKL_HIPCHECK(hipStreamSynchronize(s));
 }
 
 // src != nullptr (first DIT pass of an LDE): element i of column c is read from
@@ -953,14 +963,36 @@ void set_ntt_lazy(bool on) { g_ntt_lazy.store(on ? 1 : 0); }
 
 static int ilog2s(size_t n) { int k = 0; while (((size_t)1 << k) < n) k++; return k; }
 
+// Stage split of one transform into LDS passes.  The pass over the largest stride S (the
+// last DIT pass, the first DIF pass) takes at most 7 stages, so a workgroup owns G = 8
+// consecutive L = 128 contiguous bytes of every row it touches (full cache lines: with 4
+// consecutive L a line was split between two workgroups on different XCDs and fetched twice);
+// the other passes take up to 9 stages (the lazy kernel's limbs stay below 2^31 for 9 stages:
+// 2^26 + 9 * 2^27).  16 LDE stages = 9 + 7, 15 = 8 + 7.
+static std::vector<int> ntt_split(int K) {
+  std::vector<int> rs;
+  if (K <= 0) return rs;
+  if (K <= 9) { rs.push_back(K); return rs; }
+  int rest = K - 7;
+  const int np = (rest + 8) / 9;
+  for (int i = 0; i < np; i++) {
+    const int r = (rest + (np - i) - 1) / (np - i);
+    rs.push_back(r);
+    rest -= r;
+  }
+  rs.push_back(7);  // ascending-S order (DIT); DIF walks it backwards
+  return rs;
+}
+
 static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, MontTab roots, size_t Ntab,
                        const fe* src, int src_logb, hipStream_t s) {
   int logN = ilog2s(N), logTab = ilog2s(Ntab);
   if (hi < lo) return;
+  const std::vector<int> rs = ntt_split(hi - lo + 1);
   if (dif) {
     int cur = hi;
-    while (cur >= lo) {
-      int r = std::min(8, cur - lo + 1);
+    for (size_t k = rs.size(); k-- > 0;) {
+      const int r = rs[k];
       int logS = cur - r + 1;
       size_t groups = (N >> r) * ncols;
       size_t G = NTT_ELEMS >> r;
@@ -970,8 +1002,7 @@ static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
     }
   } else {
     int cur = lo;
-    while (cur <= hi) {
-      int r = std::min(8, hi - cur + 1);
+    for (const int r : rs) {
       size_t groups = (N >> r) * ncols;
       size_t G = NTT_ELEMS >> r;
       if (ntt_lazy_enabled())
@@ -994,7 +1025,7 @@ void launch_lde_from_coeffs(const fe* d_coef, size_t ncols, size_t n, size_t N, 
                             hipStream_t s) {
   const int logB = ilog2s(N / n);
   if (logB == 0) {
-    (void)hipMemcpyAsync(d_out, d_coef, ncols * n * sizeof(fe), hipMemcpyDeviceToDevice, s);
+    ZKL_HIPCHECK(hipMemcpyAsync(d_out, d_coef, ncols * n * sizeof(fe), hipMemcpyDeviceToDevice, s));
     ntt_passes(d_out, ncols, N, false, 0, ilog2s(N) - 1, roots, Ntab, nullptr, 0, s);
     return;
   }
@@ -1415,7 +1446,7 @@ static void launch_coset_inv(const fe* d_roots, int shift, size_t M, fe a1, fe a
 void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab, const fe* d_bm,
                             const CeParams& p, ProofConsts* dK, bool pose_block, bool ram_merkle, fe* d_xinv, fe* d_out,
                             hipStream_t s) {
-  (void)hipMemcpyAsync(&dK->ce, &p, sizeof p, hipMemcpyHostToDevice, s);
+  ZKL_HIPCHECK(hipMemcpyAsync(&dK->ce, &p, sizeof p, hipMemcpyHostToDevice, s));
   int shift = ilog2s(Ntab) - ilog2s(p.ce);
   launch_coset_inv(d_roots, shift, p.ce, p.gl, fe_zero(), 0, d_xinv, s);  // 1 / (x - g^(n-1))
   const unsigned grid = (unsigned)((p.ce + 255) / 256);

@@ -33,14 +33,8 @@ void children_root(const uint8_t suite[32], const uint8_t* digests, const uint8_
 
 namespace {
 
-#define HIPCHECK(x)                                                                           \
-  do {                                                                                        \
-    hipError_t e_ = (x);                                                                      \
-    if (e_ != hipSuccess)                                                                     \
-      throw DeviceError(std::string(#x) + ": " + hipGetErrorString(e_));                      \
-  } while (0)
+#define HIPCHECK(x) ZKL_HIPCHECK(x)
 
-struct DeviceError : std::runtime_error { using std::runtime_error::runtime_error; };
 struct InvalidArg : std::runtime_error { using std::runtime_error::runtime_error; };
 
 int ilog2(size_t n) { int k = 0; while (((size_t)1 << k) < n) k++; return k; }
@@ -213,14 +207,14 @@ struct KScope {
     if (C->evnext + 2 > C->evpool.size()) {
       size_t old = C->evpool.size();
       C->evpool.resize(old + 256);
-      for (size_t k = old; k < C->evpool.size(); k++) (void)hipEventCreate(&C->evpool[k]);
+      for (size_t k = old; k < C->evpool.size(); k++) HIPCHECK(hipEventCreate(&C->evpool[k]));
     }
     i = C->evnext;
     C->evnext += 2;
     C->kmarks.push_back({fam, i});
-    (void)hipEventRecord(C->evpool[i], C->stream);
+    HIPCHECK(hipEventRecord(C->evpool[i], C->stream));
   }
-  ~KScope() {
+  ~KScope() {  // a failed stop record shows up as an error of hipEventElapsedTime in resolve_kernel_times
     if (i != SIZE_MAX) (void)hipEventRecord(C->evpool[i + 1], C->stream);
   }
 };
@@ -229,7 +223,7 @@ void resolve_kernel_times(zkl_ctx* C) {
   for (int f = 0; f < ZKL_NUM_KFAMILIES; f++) { C->kfam_ms[f] = 0; C->kfam_n[f] = 0; }
   for (auto& m : C->kmarks) {
     float ms = 0;
-    (void)hipEventElapsedTime(&ms, C->evpool[m.second], C->evpool[m.second + 1]);
+    HIPCHECK(hipEventElapsedTime(&ms, C->evpool[m.second], C->evpool[m.second + 1]));
     C->kfam_ms[m.first] += ms;
     C->kfam_n[m.first]++;
   }
@@ -308,13 +302,13 @@ struct StageTimer {
     }
   }
   void mark(int i) {
-    if (inner || i == 0 || i == ZKL_NUM_STAGES) (void)hipEventRecord(ev[i], C->stream);
+    if (inner || i == 0 || i == ZKL_NUM_STAGES) HIPCHECK(hipEventRecord(ev[i], C->stream));
   }
   void finish() {
-    (void)hipEventSynchronize(ev[ZKL_NUM_STAGES]);
+    HIPCHECK(hipEventSynchronize(ev[ZKL_NUM_STAGES]));
     for (int i = 0; i < ZKL_NUM_STAGES; i++) {
       float ms = 0;
-      if (inner) (void)hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+      if (inner) HIPCHECK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
       C->stage_ms[i] = ms;
     }
   }
@@ -343,10 +337,10 @@ __global__ void powers_kernel(fe base, fe mult, size_t n, int logn, fe* out) {
   out[j] = fe_mul(mult, fe_pow64(base, k));
 }
 
-void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t W, uint32_t n32,
-                const zkl_air_public_inputs& pi, const zkl_proof_options& o, std::vector<uint8_t>& out) {
-  const auto t_call0 = std::chrono::steady_clock::now();
-  hipStream_t s = C->stream;
+// Request checks that need no device (winterfell ProofOptions / PartitionOptions bounds, the
+// options this backend supports, the public-input shape).  Shared by the prover and
+// zkl_hip_check_request.
+void validate_request(uint32_t W, uint32_t n32, const zkl_air_public_inputs& pi, const zkl_proof_options& o) {
   const size_t n = n32;
   if (n < 32 || (n & (n - 1))) throw InvalidArg("trace length must be a power of two >= 32");
   if (o.field_extension != 1) throw InvalidArg("only FieldExtension::None is supported for segment proofs");
@@ -354,12 +348,26 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   if (o.batching_constraints != 0 || o.batching_deep != 0) throw InvalidArg("only BatchingMethod::Linear is supported");
   if (o.blowup_factor < 2 || (o.blowup_factor & (o.blowup_factor - 1))) throw InvalidArg("blowup must be a power of two");
   if (o.num_queries == 0 || o.num_queries > 255) throw InvalidArg("num_queries must be in 1..255");
+  // winter-air PartitionOptions::new bounds (num_partitions 1..=16, min_partition_size 1..=256)
+  if (o.num_partitions < 1 || o.num_partitions > 16) throw InvalidArg("num_partitions must be in 1..16");
+  if (o.hash_rate < 1 || o.hash_rate > 256) throw InvalidArg("hash_rate must be in 1..256");
+  if (o.fri_remainder_max_degree > 15 || ((o.fri_remainder_max_degree + 1) & o.fri_remainder_max_degree))
+    throw InvalidArg("fri_remainder_max_degree must be one less than a power of two, at most 15");
+  if (pi.n_main_slots > ZKL_MAX_MAIN_SLOTS) throw InvalidArg("n_main_slots exceeds ZKL_MAX_MAIN_SLOTS");
+  if (W == 0 || W > 4096) throw InvalidArg("trace width must be in 1..4096");
+}
+
+void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t W, uint32_t n32,
+                const zkl_air_public_inputs& pi, const zkl_proof_options& o, std::vector<uint8_t>& out) {
+  const auto t_call0 = std::chrono::steady_clock::now();
+  hipStream_t s = C->stream;
+  const size_t n = n32;
+  validate_request(W, n32, pi, o);
   const size_t N = n * o.blowup_factor;
   const int logn = ilog2(n), logN = ilog2(N);
   const uint32_t B = o.blowup_factor;
   const fe g = root_of_unity(logn), three{3, 0};
   const Hasher& H = hasher();
-  if (W == 0 || W > 4096) throw InvalidArg("trace width must be in 1..4096");
 
   upload_hasher(s);
   ensure_tables(C, n, N);
@@ -382,19 +390,21 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     launch_scale_bitrev(C->coef.f(), W, n, C->opow_n.f(), s);                  // -> c_k * 3^k (coset shift)
     launch_lde_from_coeffs(C->coef.f(), W, n, N, mroots, Ntab, C->lde.f(), s);
   }
+  check_launch("trace LDE");
   T.mark(1);
   // ---- trace commitment (commit_to_rows + MerkleTree)
-  uint32_t np_tr = o.num_partitions ? o.num_partitions : 1;
-  C->parts.ensure((size_t)std::max<uint32_t>(np_tr, 1) * N * sizeof(fe) + N * sizeof(fe));
+  C->parts.ensure((size_t)o.num_partitions * N * sizeof(fe) + N * sizeof(fe));
   C->tree.ensure(2 * N * sizeof(fe));
   {
     KScope k(C, KF_TRACE_HASH);
     launch_hash_rows(C->lde.f(), W, N, o.num_partitions, o.hash_rate, C->parts.f(), C->tree.f() + N, s);
   }
+  check_launch("trace row hash");
   {
     KScope k(C, KF_MERKLE);
     launch_merkle(C->tree.f(), N, s);
   }
+  check_launch("trace Merkle tree");
   // ---- coin seed: Context::to_elements || AirPublicInputs::to_elements (agg/fs.rs:67-73),
   // hashed on the host while the device runs the trace LDE and commitment queued above
   std::vector<fe> seed_el = context_elements(W, n, o);
@@ -471,6 +481,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     KScope k(C, KF_MISC);
     launch_draws(coin.seed, coin.counter, ndraw, C->draws.f(), s);
   }
+  check_launch("composition coefficient draws");
   coin.counter += ndraw;
   upload_alphas_from_device(dK, C->draws.f(), air.n_tc, s);
 
@@ -487,6 +498,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     launch_broadcast(C->bvec.f(), n, 1, 0, nb + 1, n, ce, C->opow.f(), fe_one(), true, C->bm.f(), s);
     launch_ntt_stages(C->bm.f(), nb + 1, ce, false, ilog2(ce / n), logce - 1, mroots, Ntab, s);
   }
+  check_launch("boundary tables");
 
   // periodic table
   if (C->pert_key_n != n || C->pert_key_ce != ce) {
@@ -519,6 +531,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     launch_constraint_eval(C->lde.f(), roots, Ntab, C->pertab.f(), C->bm.f(), cp, dK, air.dev.pose_block != 0,
                            (air.dev.ram_block | air.dev.merkle_block) != 0, C->xinv.f(), C->ce.f(), s);
   }
+  check_launch("constraint evaluation");
   T.mark(3);
 
   // ---- 3. composition polynomial: coset interpolation, degree check, column LDE, commit
@@ -539,6 +552,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     }
     launch_ntt_stages(C->clde.f(), Cc, N, false, ilog2(B), logN - 1, mroots, Ntab, s);
   }
+  check_launch("composition polynomial LDE");
   C->ctree.ensure(2 * N * sizeof(fe));
   {
     KScope k(C, KF_COMP_HASH);
@@ -548,6 +562,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     KScope k(C, KF_MERKLE);
     launch_merkle(C->ctree.f(), N, s);
   }
+  check_launch("composition commitment");
   unsigned bad = 0;
   d2h(C, &bad, C->flag.p, 4);
   if (bad) throw InvalidArg("constraint composition polynomial degree too large: trace does not satisfy the AIR");
@@ -582,6 +597,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     for (int j = 0; j < Cc; j++) b.off[j] = bitrev_u((uint32_t)j, loge);
     launch_ood(b, dood + n_otr, s);
   }
+  check_launch("OOD evaluation");
   std::vector<fe> hood(2 * ((size_t)W + Cc), fe_zero());
   C->h_ood.ensure((n_otr + n_ocp) * sizeof(fe));
   const fe* part = C->h_ood.at<fe>();
@@ -594,6 +610,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     KScope k(C, KF_DEEP);
     launch_deep_denoms(roots, Ntab, N, z, zg, C->xinv.f(), s);
   }
+  check_launch("DEEP denominators");
   HT("ood_enqueued");
   HIPCHECK(hipEventSynchronize(C->hev));
   // hood = t(z) [W] | t(zg) [W] | chat(z) [Cc] | chat(zg) [Cc]
@@ -624,6 +641,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   HT("ood_hashed");
   std::vector<fe> gam(W + Cc);
   launch_draws(coin.seed, coin.counter, W + Cc, C->draws.f(), s);
+  check_launch("DEEP coefficient draws");
   coin.counter += W + Cc;
   d2h(C, gam.data(), C->draws.p, gam.size() * sizeof(fe));
   HT("gam");
@@ -638,6 +656,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     KScope k(C, KF_DEEP);
     launch_deep(C->lde.f(), C->clde.f(), roots, Ntab, dp, dK, C->xinv.f(), C->deep.f(), s);
   }
+  check_launch("DEEP composition");
   T.mark(6);
 
   // ---- 6. FRI (FriProver::build_layers, folding 2, remainder degree rem_deg)
@@ -675,6 +694,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     launch_fri_coin(d_coin, tr + 1, d_coin + 2 + d, s);
     launch_fri_fold(layer_ev(d), Nd, d_coin + 1, iroots, Ntab, layer_ev(d + 1), s);
   }
+  check_launch("FRI layers");
   HT("fri_enqueued");
   if (nl > 0) {
     std::vector<fe> cs(2 + (size_t)nl);
@@ -717,6 +737,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
       HIPCHECK(hipMemcpyAsync(C->best.p, &init, 8, hipMemcpyHostToDevice, s));
       KScope k(C, KF_GRIND);
       launch_grind(coin.seed, base, batch, o.grinding_factor, (unsigned long long*)C->best.p, s);
+      check_launch("grinding");
       unsigned long long r = 0;
       d2h(C, &r, C->best.p, 8);
       if (r != ~0ull) nonce = r;
@@ -730,6 +751,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   coin.counter = 0;
   std::vector<fe> qd(o.num_queries);
   launch_draws(coin.seed, 0, o.num_queries, C->draws.f(), s);
+  check_launch("query draws");
   d2h(C, qd.data(), C->draws.p, qd.size() * sizeof(fe));
   HT("q_drawn");
   std::vector<size_t> pos;
@@ -773,6 +795,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   memcpy(C->h_addr.p, addrs.data(), na_g * 8);
   HIPCHECK(hipMemcpyAsync(C->gaddr.p, C->h_addr.p, na_g * 8, hipMemcpyHostToDevice, s));
   launch_gather((const uint64_t*)C->gaddr.p, na_g, C->gout.f(), s);
+  check_launch("query gather");
   HIPCHECK(hipMemcpyAsync(C->h_gv.p, C->gout.p, na_g * sizeof(fe), hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
   HT("q_gathered");
@@ -843,7 +866,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->host_ms[2] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call0).count();
   {
     float gpu_ms = 0;
-    (void)hipEventElapsedTime(&gpu_ms, T.ev[0], T.ev[ZKL_NUM_STAGES]);
+    HIPCHECK(hipEventElapsedTime(&gpu_ms, T.ev[0], T.ev[ZKL_NUM_STAGES]));
     C->host_ms[1] = C->host_ms[2] - C->host_ms[0] - gpu_ms;  // host time not overlapped by the stream
   }
 }
@@ -947,6 +970,18 @@ int zkl_hip_prove_segment_device(zkl_ctx* c, const void* d_trace, uint32_t width
   return rc ? rc : finish_proof(v, proof, len);
 }
 
+int zkl_hip_check_request(uint32_t width, uint32_t n_rows, const zkl_air_public_inputs* pi,
+                          const zkl_proof_options* o) {
+  if (!pi || !o) return ZKL_E_INVALID;
+  return run_guarded(nullptr, [&] {
+    validate_request(width, n_rows, *pi, *o);
+    AirInstance air;
+    std::string e = build_air(*pi, width, n_rows, air);
+    if (e.empty() && o->blowup_factor < (uint32_t)air.ce_blowup) e = "blowup factor below constraint-evaluation blowup";
+    if (!e.empty()) throw InvalidArg(e);
+  });
+}
+
 int zkl_hip_host_times(const zkl_ctx* c, double* out_ms, int max_n) {
   if (!c || !out_ms) return ZKL_E_INVALID;
   int k = std::min(max_n, 3);
@@ -1048,13 +1083,14 @@ void zkl_select_partitions(uint32_t w, uint32_t len, uint32_t* parts, uint32_t* 
 }
 
 int zkl_hip_hash_rows(zkl_ctx* c, const void* d_m, uint32_t nc, uint32_t nr, uint32_t np, uint32_t rate, void* d_out) {
-  if (!c) return ZKL_E_INVALID;
+  if (!c || !d_m || !d_out || nc == 0 || np < 1 || np > 16 || rate < 1 || rate > 256) return ZKL_E_INVALID;
   std::lock_guard<std::mutex> lk(c->mu);
   return run_guarded(c, [&] {
     HIPCHECK(hipSetDevice(c->device));
     upload_hasher(c->stream);
     c->parts.ensure((size_t)std::max<uint32_t>(np, 1) * nr * sizeof(fe) + 16);
     launch_hash_rows((const fe*)d_m, nc, nr, np, rate, c->parts.f(), (fe*)d_out, c->stream);
+    check_launch("stage entry point");
     HIPCHECK(hipStreamSynchronize(c->stream));
   });
 }
@@ -1064,6 +1100,14 @@ int zkl_hip_set_ntt_mode(int lazy) {
   set_ntt_lazy(lazy != 0);
   return 0;
 }
+
+int zkl_hip_set_row_digest_rule(int rule) {
+  if (rule < 0 || rule > 1) return ZKL_E_INVALID;
+  set_row_digest_rule(rule);
+  return 0;
+}
+
+int zkl_hip_row_digest_rule(void) { return row_digest_rule(); }
 
 int zkl_hip_set_hash_policy(int engine, uint32_t pm_min_items) {
   if (engine < 0 || engine > 1) return ZKL_E_INVALID;
@@ -1078,6 +1122,7 @@ int zkl_hip_poseidon_permute(zkl_ctx* c, void* d_states, uint32_t n_states, int 
     HIPCHECK(hipSetDevice(c->device));
     upload_hasher(c->stream);
     launch_permute((fe*)d_states, n_states, engine, c->stream);
+    check_launch("stage entry point");
     HIPCHECK(hipStreamSynchronize(c->stream));
   });
 }
@@ -1091,6 +1136,7 @@ int zkl_hip_merkle_tree(zkl_ctx* c, const void* d_leaves, uint32_t n, void* d_no
     HIPCHECK(hipMemcpyAsync((fe*)d_nodes + n, d_leaves, (size_t)n * sizeof(fe), hipMemcpyDeviceToDevice, c->stream));
     HIPCHECK(hipMemsetAsync(d_nodes, 0, sizeof(fe), c->stream));
     launch_merkle((fe*)d_nodes, n, c->stream);
+    check_launch("stage entry point");
     HIPCHECK(hipStreamSynchronize(c->stream));
   });
 }
@@ -1103,6 +1149,7 @@ int zkl_hip_ntt(zkl_ctx* c, void* d_data, uint32_t nc, uint32_t n, int dif, int 
     ensure_tables(c, c->tab_n ? c->tab_n : n, std::max<size_t>(n, c->tab_N));
     const MontTab t = mont_tab(inverse ? c->miroots.p : c->mroots.p, c->tab_N);
     launch_ntt_stages((fe*)d_data, nc, n, dif != 0, 0, ilog2(n) - 1, t, c->tab_N, c->stream);
+    check_launch("stage entry point");
     HIPCHECK(hipStreamSynchronize(c->stream));
   });
 }
@@ -1121,6 +1168,7 @@ int zkl_hip_lde(zkl_ctx* c, const void* d_values, uint32_t nc, uint32_t n, uint3
     launch_ntt_stages(coef, nc, n, true, 0, ilog2(n) - 1, mont_tab(c->miroots.p, c->tab_N), c->tab_N, s);
     launch_scale_bitrev(coef, nc, n, c->opow_n.f(), s);
     launch_lde_from_coeffs(coef, nc, n, N, mont_tab(c->mroots.p, c->tab_N), c->tab_N, (fe*)d_lde, s);
+    check_launch("stage entry point");
     // return natural-order coefficients: scale n*c (bitrev) by 1/n and un-permute on host side is
     // not needed by callers; convert in place to natural order here
     std::vector<fe> h((size_t)nc * n), r((size_t)nc * n);

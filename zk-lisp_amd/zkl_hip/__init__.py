@@ -16,7 +16,7 @@ __all__ = [
     "F128", "ProofOptions", "AirPublicInputs", "ZklError", "Context", "load_library",
     "select_partitions_for_trace", "proof_options", "synth_vm_segment", "STAGE_NAMES",
     "FM_VM", "FM_VM_EXPECT", "FM_POSEIDON", "FM_SPONGE", "FM_MERKLE", "FM_RAM",
-    "VmArg", "StepInfo", "step_proof_encode", "step_proof_digest", "parse_step_proof", "children_root",
+    "VmArg", "StepInfo", "check_request", "row_digest_rule", "step_proof_encode", "step_proof_digest", "parse_step_proof", "children_root",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -142,6 +142,8 @@ def load_library():
     lib.zkl_hip_poseidon_permute.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int]
     lib.zkl_hip_set_hash_policy.argtypes = [C.c_int, C.c_uint32]
     lib.zkl_hip_set_ntt_mode.argtypes = [C.c_int]
+    lib.zkl_hip_set_row_digest_rule.argtypes = [C.c_int]
+    lib.zkl_hip_check_request.argtypes = [C.c_uint32, C.c_uint32, P(AirPublicInputs), P(ProofOptions)]
     lib.zkl_hip_set_kernel_timing.argtypes = [C.c_void_p, C.c_int]
     lib.zkl_step_proof_encode.argtypes = [P(AirPublicInputs), P(StepInfo), C.c_char_p, C.c_size_t,
                                           P(P(C.c_uint8)), P(C.c_size_t)]
@@ -150,6 +152,34 @@ def load_library():
     lib.zkl_hip_lde.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]
     _lib = lib
     return lib
+
+
+def check_request(width: int, n_rows: int, pi: AirPublicInputs, opts: ProofOptions) -> None:
+    """The prover's request checks without a device (zkl_hip_check_request); raises ZklError
+    with the prover's message, as prove_segment would before any device work."""
+    lib = load_library()
+    rc = lib.zkl_hip_check_request(width, n_rows, C.byref(pi), C.byref(opts))
+    if rc != 0:
+        raise ZklError(rc, lib.zkl_hip_last_error(None).decode(errors="replace"))
+
+
+class row_digest_rule:
+    """Context manager selecting the one-chunk row-digest rule (zkl_hip_set_row_digest_rule):
+    0 winterfell commit_to_rows (default), 1 agg/child.rs:1025-1045 hash_row_poseidon."""
+
+    def __init__(self, rule: int):
+        self.rule = rule
+
+    def __enter__(self):
+        lib = load_library()
+        self.prev = lib.zkl_hip_row_digest_rule()
+        if lib.zkl_hip_set_row_digest_rule(self.rule) != 0:
+            raise ZklError(-1, f"invalid row digest rule {self.rule}")
+        return self
+
+    def __exit__(self, *exc):
+        load_library().zkl_hip_set_row_digest_rule(self.prev)
+        return False
 
 
 def device_count() -> int:
