@@ -226,6 +226,16 @@ int zkl_hip_lde(zkl_ctx* ctx, const void* d_values, uint32_t n_cols, uint32_t n_
  * scaling.  out[k] = sum_j in[j] * w^(j*k) in the respective orders. */
 int zkl_hip_ntt(zkl_ctx* ctx, void* d_data, uint32_t n_cols, uint32_t n, int dif, int inverse);
 
+/* ---- verification (host, no device work) ------------------------------------
+ * winter-verifier 0.13.1 for one segment proof (verify_proof, prove.rs:802-941): context and
+ * options (must equal opts), commitments, transcript replay (agg/fs.rs:67-237), the
+ * out-of-domain constraint identity (transition constraints of ZkLispAir + every assertion),
+ * proof of work, query positions, trace / constraint / FRI Merkle openings, DEEP values, FRI
+ * folds and remainder.  ZKL_OK when the proof verifies; ZKL_E_INVALID with
+ * zkl_hip_last_error(NULL) naming the first failing check otherwise. */
+int zkl_verify_segment(const uint8_t* proof, size_t len, const zkl_air_public_inputs* pi,
+                       const zkl_proof_options* opts);
+
 /* ---- workload generator (host, not the measured path) -------------------- */
 /* Synthetic VM-only straight-line segment: 2^log_n rows, width 204
  * ({vm, rom} layout), ops cycling Const/Add/Mov/Mul over r0..r7 with splitmix64

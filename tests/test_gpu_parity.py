@@ -565,6 +565,7 @@ def test_headline_proof_matches_golden(gpu_ctx, name):
     got = gpu_ctx.prove_segment(t, w, n, pi, opts)
     assert len(got) == g["len"]
     assert hashlib.sha256(got).hexdigest() == g["sha256"]
+    zkl_hip.verify_segment(got, pi, opts)  # product-side verifier (zkl_verify_segment)
 
 
 def test_headline_proof_equals_oracle_proof(oracle, gpu_ctx):

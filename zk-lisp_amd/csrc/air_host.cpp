@@ -270,42 +270,58 @@ std::vector<fe> context_elements(uint32_t width, size_t n, const zkl_proof_optio
           fe{o.grinding_factor, 0}, fe{o.blowup_factor, 0}, fe{o.num_queries, 0}};
 }
 
-std::vector<fe> periodic_table(size_t n, size_t ce, fe offset) {
-  // q_col(y) interpolates the column's 32 values over <w_32>; coefficients by inverse DFT
-  fe w32 = root_of_unity(5), w32i = fe_inv(w32), inv32 = fe_inv(fe{32, 0});
-  std::vector<fe> coef(31 * 32);
+// coefficients (over y, degree < 32) of the 31 cycle-32 selector columns: q_col(y)
+// interpolates the column's 32 values over <w_32> (inverse DFT)
+static const std::vector<fe>& periodic_coeffs() {
+  static const std::vector<fe> coef = [] {
+    fe w32 = root_of_unity(5), w32i = fe_inv(w32), inv32 = fe_inv(fe{32, 0});
+    std::vector<fe> c(31 * 32);
+    for (int col = 0; col < 31; col++) {
+      fe v[32];
+      for (int pos = 0; pos < 32; pos++) {
+        bool one;
+        if (col == 0) one = pos == 0;
+        else if (col <= 27) one = pos == col;
+        else if (col == 28) one = pos == 28;
+        else if (col == 29) one = pos >= 29;
+        else one = pos == 31;
+        v[pos] = one ? fe_one() : fe_zero();
+      }
+      for (int k = 0; k < 32; k++) {
+        fe acc = fe_zero(), wk = fe_pow64(w32i, k), pw = fe_one();
+        for (int j = 0; j < 32; j++) { acc = fe_add(acc, fe_mul(v[j], pw)); pw = fe_mul(pw, wk); }
+        c[col * 32 + k] = fe_mul(acc, inv32);
+      }
+    }
+    return c;
+  }();
+  return coef;
+}
+
+static void periodic_eval(size_t n, fe x, fe* out) {
+  const std::vector<fe>& coef = periodic_coeffs();
+  const fe y = fe_pow64(x, n / 32);
   for (int col = 0; col < 31; col++) {
-    fe v[32];
-    for (int pos = 0; pos < 32; pos++) {
-      bool one;
-      if (col == 0) one = pos == 0;
-      else if (col <= 27) one = pos == col;
-      else if (col == 28) one = pos == 28;
-      else if (col == 29) one = pos >= 29;
-      else one = pos == 31;
-      v[pos] = one ? fe_one() : fe_zero();
-    }
-    for (int k = 0; k < 32; k++) {
-      fe acc = fe_zero(), wk = fe_pow64(w32i, k), pw = fe_one();
-      for (int j = 0; j < 32; j++) { acc = fe_add(acc, fe_mul(v[j], pw)); pw = fe_mul(pw, wk); }
-      coef[col * 32 + k] = fe_mul(acc, inv32);
-    }
+    fe acc = fe_zero();
+    for (int k = 31; k >= 0; k--) acc = fe_add(fe_mul(acc, y), coef[col * 32 + k]);
+    out[col] = acc;
   }
+}
+
+std::vector<fe> periodic_table(size_t n, size_t ce, fe offset) {
   unsigned logce = 0;
   while (((size_t)1 << logce) < ce) logce++;
   fe wce = root_of_unity(logce);
   size_t period = ce / (n / 32);
   std::vector<fe> tab(period * 31);
-  for (size_t i = 0; i < period; i++) {
-    fe x = fe_mul(offset, fe_pow64(wce, i));
-    fe y = fe_pow64(x, n / 32);
-    for (int col = 0; col < 31; col++) {
-      fe acc = fe_zero();
-      for (int k = 31; k >= 0; k--) acc = fe_add(fe_mul(acc, y), coef[col * 32 + k]);
-      tab[i * 31 + col] = acc;
-    }
-  }
+  for (size_t i = 0; i < period; i++) periodic_eval(n, fe_mul(offset, fe_pow64(wce, i)), &tab[i * 31]);
   return tab;
+}
+
+std::vector<fe> periodic_at(size_t n, fe x) {
+  std::vector<fe> v(31);
+  periodic_eval(n, x, v.data());
+  return v;
 }
 
 }  // namespace zkl

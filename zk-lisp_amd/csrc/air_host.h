@@ -71,6 +71,8 @@ std::vector<fe> context_elements(uint32_t width, size_t n, const zkl_proof_optio
 // Periodic cycle-32 selector values p_map, p_r[27], p_final, p_pad, p_pad_last evaluated at
 // y = x^(n/32) for the 256 distinct y of the CE coset: table[256][31] (vm/air/mod.rs:520-592).
 std::vector<fe> periodic_table(size_t n, size_t ce_size, fe offset);
+// the same 31 values at one point x (the verifier's out-of-domain point)
+std::vector<fe> periodic_at(size_t n, fe x);
 
 fe fe_from(const zkl_f128& v);
 zkl_f128 to_abi(fe v);

@@ -82,7 +82,7 @@ __host__ __device__ inline fe fe_neg(fe a) { return fe_sub(fe_zero(), a); }
 
 // ---------------------------------------------------------------- device multiply
 // 128x128 -> 256 schoolbook on 32-bit limbs: 16 v_mad_u64_u32.
-__device__ inline void mul_wide32(fe a, fe b, uint32_t r[8]) {
+__host__ __device__ inline void mul_wide32(fe a, fe b, uint32_t r[8]) {
   uint32_t x[4] = {(uint32_t)a.lo, (uint32_t)(a.lo >> 32), (uint32_t)a.hi, (uint32_t)(a.hi >> 32)};
   uint32_t y[4] = {(uint32_t)b.lo, (uint32_t)(b.lo >> 32), (uint32_t)b.hi, (uint32_t)(b.hi >> 32)};
 #pragma unroll
@@ -102,7 +102,7 @@ __device__ inline void mul_wide32(fe a, fe b, uint32_t r[8]) {
 
 // reduce a 288-bit value r[0..9) (r[8] small) modulo p.
 // x = H*2^128 + L ; 2^128 == 45*2^40 - 1.
-__device__ inline fe reduce288(const uint32_t r[9]) {
+__host__ __device__ inline fe reduce288(const uint32_t r[9]) {
   // H = r[4..9) (up to 160 bits), T = 45*H
   uint32_t T[6];
   uint64_t c = 0;
@@ -193,7 +193,7 @@ __device__ inline fe reduce288(const uint32_t r[9]) {
 
 
 // acc[0..9) += a*b (lazy accumulation for dot products, <= 2^32 terms)
-__device__ inline void mul_acc(fe a, fe b, uint32_t acc[9]) {
+__host__ __device__ inline void mul_acc(fe a, fe b, uint32_t acc[9]) {
   uint32_t r[8];
   mul_wide32(a, b, r);
   uint64_t c = 0;

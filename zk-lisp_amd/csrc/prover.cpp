@@ -21,6 +21,7 @@
 #include "air_host.h"
 #include "host_hash.h"
 #include "kernels.h"
+#include "proof_view.h"
 
 using namespace zkl;
 
@@ -978,6 +979,15 @@ int zkl_hip_check_request(uint32_t width, uint32_t n_rows, const zkl_air_public_
     AirInstance air;
     std::string e = build_air(*pi, width, n_rows, air);
     if (e.empty() && o->blowup_factor < (uint32_t)air.ce_blowup) e = "blowup factor below constraint-evaluation blowup";
+    if (!e.empty()) throw InvalidArg(e);
+  });
+}
+
+int zkl_verify_segment(const uint8_t* proof, size_t len, const zkl_air_public_inputs* pi,
+                       const zkl_proof_options* opts) {
+  if (!proof || !pi || !opts) return ZKL_E_INVALID;
+  return run_guarded(nullptr, [&] {
+    const std::string e = verify_segment(proof, len, *pi, *opts, nullptr);
     if (!e.empty()) throw InvalidArg(e);
   });
 }

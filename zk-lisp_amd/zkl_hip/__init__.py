@@ -16,7 +16,7 @@ __all__ = [
     "F128", "ProofOptions", "AirPublicInputs", "ZklError", "Context", "load_library",
     "select_partitions_for_trace", "proof_options", "synth_vm_segment", "STAGE_NAMES",
     "FM_VM", "FM_VM_EXPECT", "FM_POSEIDON", "FM_SPONGE", "FM_MERKLE", "FM_RAM",
-    "VmArg", "StepInfo", "check_request", "row_digest_rule", "step_proof_encode", "step_proof_digest", "parse_step_proof", "children_root",
+    "VmArg", "StepInfo", "check_request", "row_digest_rule", "verify_segment", "step_proof_encode", "step_proof_digest", "parse_step_proof", "children_root",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -143,6 +143,7 @@ def load_library():
     lib.zkl_hip_set_hash_policy.argtypes = [C.c_int, C.c_uint32]
     lib.zkl_hip_set_ntt_mode.argtypes = [C.c_int]
     lib.zkl_hip_set_row_digest_rule.argtypes = [C.c_int]
+    lib.zkl_verify_segment.argtypes = [C.c_char_p, C.c_size_t, P(AirPublicInputs), P(ProofOptions)]
     lib.zkl_hip_check_request.argtypes = [C.c_uint32, C.c_uint32, P(AirPublicInputs), P(ProofOptions)]
     lib.zkl_hip_set_kernel_timing.argtypes = [C.c_void_p, C.c_int]
     lib.zkl_step_proof_encode.argtypes = [P(AirPublicInputs), P(StepInfo), C.c_char_p, C.c_size_t,
@@ -159,6 +160,15 @@ def check_request(width: int, n_rows: int, pi: AirPublicInputs, opts: ProofOptio
     with the prover's message, as prove_segment would before any device work."""
     lib = load_library()
     rc = lib.zkl_hip_check_request(width, n_rows, C.byref(pi), C.byref(opts))
+    if rc != 0:
+        raise ZklError(rc, lib.zkl_hip_last_error(None).decode(errors="replace"))
+
+
+def verify_segment(proof: bytes, pi: AirPublicInputs, opts: ProofOptions) -> None:
+    """winter-verifier checks of one segment proof on the host (zkl_verify_segment; the
+    reference's verify_proof, prove.rs:802-941).  Raises ZklError naming the failing check."""
+    lib = load_library()
+    rc = lib.zkl_verify_segment(bytes(proof), len(proof), C.byref(pi), C.byref(opts))
     if rc != 0:
         raise ZklError(rc, lib.zkl_hip_last_error(None).decode(errors="replace"))
 
