@@ -79,6 +79,37 @@ int main() {
         if (!fe_eq(mul_tw(a, t, 0), fe_mul(a, w))) { if (bad++ < 10) printf("mul_tw mismatch\n"); }
     }
   }
+  // R' = 2^130 helpers of the matrix-core permutation: cubes of values < 2^129 (normalised
+  // limbs, the round invariant) stay < 2^129; cubes of sums of two such values (< 2^130, a
+  // state element after absorbing a message) stay < 2^131; extreme limb patterns included
+  {
+    const fe R1 = fe_pow64(fe{2, 0}, 130), R1inv = fe_inv(R1);
+    auto val_bits_ok = [](const uint32_t l[5], int bits) {  // normalised limbs, value < 2^bits
+      for (int j = 0; j < 4; j++)
+        if (l[j] >= (1u << 26)) return false;
+      return l[4] < (1u << (bits - 104));
+    };
+    for (int it = 0; it < 200000; it++) {
+      uint32_t a[5], c[5];
+      const int mode = it % 4;
+      for (int j = 0; j < 5; j++) a[j] = (uint32_t)(rng() & 0x3FFFFFF);
+      a[4] &= 0x1FFFFFF;  // < 2^129
+      if (mode == 1) { for (int j = 0; j < 4; j++) a[j] = 0x3FFFFFF; a[4] = 0x1FFFFFF; }
+      if (mode >= 2) {  // sum of two normalised values < 2^129: limbs < 2^27, value < 2^130
+        for (int j = 0; j < 5; j++) a[j] += (uint32_t)(rng() & 0x3FFFFFF) & (j == 4 ? 0x1FFFFFFu : 0x3FFFFFFu);
+        if (mode == 3) { for (int j = 0; j < 4; j++) a[j] = 0x7FFFFFE; a[4] = 0x3FFFFFE; }
+      }
+      const fe av = from26(a);
+      mont_cube130(a, c);
+      const fe want = fe_mul(fe_mul(fe_mul(av, av), av), fe_mul(R1inv, R1inv));
+      const bool bound = val_bits_ok(c, mode >= 2 ? 131 : 129);
+      if (!fe_eq(from26(c), want) || !bound) { if (bad++ < 10) printf("cube130 mismatch it=%d mode=%d\n", it, mode); }
+      uint64_t col[10] = {a[0], a[1], a[2], a[3], a[4], 0, 0, 0, 0, 0};
+      uint32_t o[5];
+      redc130(col, o);  // from_mont130: < p + 2
+      if (!fe_eq(from26(o), fe_mul(av, R1inv)) || !val_bits_ok(o, 129)) { if (bad++ < 10) printf("redc130 exit mismatch it=%d\n", it); }
+    }
+  }
   printf(bad ? "FAIL %d\n" : "OK\n", bad);
   return bad != 0;
 }

@@ -39,6 +39,11 @@ struct HasherMont {
   uint32_t dom[2][5];
   uint32_t r2[5];      // R^2 mod p (converts a canonical element into Montgomery form)
   uint32_t dfe[4][5];  // Montgomery domain labels: elements, merge, merge_many, merge_with_int
+  // the same entry constants for the matrix-core permutation, whose Montgomery radix is
+  // R' = 2^130 (five REDC digit steps instead of six; poseidon_mfma.inc)
+  uint32_t dom130[2][5];
+  uint32_t r2_130[5];  // R'^2 mod p
+  uint32_t dfe130[4][5];
 };
 HasherMont make_hasher_mont(const HasherConsts& h);
 void upload_hasher_mont(const HasherMont& m, hipStream_t s);

@@ -101,6 +101,41 @@ __host__ __device__ __forceinline__ void redc(uint64_t colu[10], uint32_t out[5]
   out[4] = (uint32_t)(v >> 26);
 }
 
+// REDC with R' = 2^130 (the matrix-core permutation's radix): five digit steps instead of
+// six.  col[0..8] = X < 2^262 (columns < 2^62); out = X * 2^-130 mod p + (0 or p), the
+// normalised limbs of a value in (0, X / 2^130 + p): inputs < 2^129 give outputs < 2^129
+// (2^258 / 2^130 + p < 2^129), inputs < 2^130 outputs < 2^131.  The bias p * 2^130 is
+// col_5 += 1, col_6 -= 737280, col_9 += 2^24; limb 4 of the output carries everything
+// above bit 104 (< 2^28).
+__host__ __device__ __forceinline__ void redc130(uint64_t colu[10], uint32_t out[5]) {
+  int64_t col[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) col[i] = (int64_t)colu[i];
+  col[5] += 1;
+  col[6] -= 737280;
+  col[9] += (int64_t)1 << 24;
+  int32_t kneg = -16777216;
+  uint32_t k45 = 737280u;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+s"(kneg), "+s"(k45));
+#endif
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    const uint32_t m = (uint32_t)col[i] & M26;
+    col[i + 1] += col[i] >> 26;
+    col[i + 1] += (int64_t)((uint64_t)m * k45);
+    col[i + 4] += (int64_t)(int32_t)m * (int64_t)kneg;
+  }
+  int64_t c = 0;
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const int64_t v = col[5 + t] + c;
+    out[t] = (uint32_t)v & M26;
+    c = v >> 26;
+  }
+  out[4] = (uint32_t)(col[9] + c);
+}
+
 __host__ __device__ __forceinline__ void mac5(const uint32_t a[5], const uint32_t b[5], uint64_t col[10]) {
 #pragma unroll
   for (int u = 0; u < 5; u++)
@@ -128,6 +163,45 @@ __host__ __device__ __forceinline__ void mont_cube(const uint32_t a[5], uint32_t
   uint32_t sq[5];
   redc(col, sq);
   mont_mul(sq, a, out);
+}
+
+// x^3 R'^-2 (R' = 2^130) with the squaring shortcut; inputs < 2^129 give outputs < 2^129,
+// inputs < 2^130 (a state element right after absorbing a message) outputs < 2^131
+__host__ __device__ __forceinline__ void mont_cube130(const uint32_t a[5], uint32_t out[5]) {
+  uint64_t col[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t d[5];
+#pragma unroll
+  for (int u = 0; u < 5; u++) d[u] = a[u] << 1;
+#pragma unroll
+  for (int u = 0; u < 5; u++) {
+    col[2 * u] += (uint64_t)a[u] * a[u];
+#pragma unroll
+    for (int v = u + 1; v < 5; v++) col[u + v] += (uint64_t)d[u] * a[v];
+  }
+  uint32_t sq[5];
+  redc130(col, sq);
+  uint64_t c2[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  mac5(sq, a, c2);
+  redc130(c2, out);
+}
+
+__device__ __forceinline__ void to_mont130(fe a, uint32_t out[5]) {
+  uint32_t l[5];
+  to26(a, l);
+  uint64_t col[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  mac5(l, c_hm.r2_130, col);
+  redc130(col, out);
+}
+
+__device__ __forceinline__ fe from_mont130(const uint32_t a[5]) {
+  uint64_t col[10] = {a[0], a[1], a[2], a[3], a[4], 0, 0, 0, 0, 0};
+  uint32_t l[5];
+  redc130(col, l);  // < p + 2
+  fe r;
+  r.lo = (uint64_t)l[0] | ((uint64_t)l[1] << 26) | ((uint64_t)l[2] << 52);
+  r.hi = ((uint64_t)l[2] >> 12) | ((uint64_t)l[3] << 14) | ((uint64_t)l[4] << 40);
+  if (r.hi == P_HI && r.lo >= P_LO) r = fe{r.lo - P_LO, 0};
+  return r;
 }
 
 __device__ __forceinline__ void to_mont(fe a, uint32_t out[5]) {
@@ -172,6 +246,15 @@ HasherMont make_hasher_mont(const HasherConsts& h) {
   mont(h.dom_merge, m.dfe[DOM_MERGE]);
   mont(h.dom_many, m.dfe[DOM_MANY]);
   mont(h.dom_int, m.dfe[DOM_INT]);
+  const fe R130 = fe_pow64(fe{2, 0}, 130);
+  auto mont130 = [&](fe x, uint32_t out[5]) { limbs26(fe_mul(x, R130), out); };
+  mont130(h.dom[0], m.dom130[0]);
+  mont130(h.dom[1], m.dom130[1]);
+  limbs26(fe_mul(R130, R130), m.r2_130);
+  mont130(h.dom_elems, m.dfe130[DOM_ELEMS]);
+  mont130(h.dom_merge, m.dfe130[DOM_MERGE]);
+  mont130(h.dom_many, m.dfe130[DOM_MANY]);
+  mont130(h.dom_int, m.dfe130[DOM_INT]);
   return m;
 }
 
@@ -826,14 +909,19 @@ __device__ __forceinline__ fe ntt_canon(const uint32_t l[5]) {
   return fe{(uint64_t)r, (uint64_t)(r >> 64)};
 }
 
+// ELEMS elements per workgroup: NTT_ELEMS, or 2 * NTT_ELEMS for a pass whose groups would
+// otherwise own only half of each 128-byte line they touch (G = ELEMS >> r < 8 consecutive L
+// at a stride S >= G: the other half went to a workgroup on another XCD and the line was
+// fetched twice -- the 8-stage top pass of the trace LDE fetched 7.1 GB for 3.4 GB)
+template <int ELEMS>
 __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restrict__ data, size_t ncols, int logN, int r,
                                                                   int logS, MontTab roots, const fe* __restrict__ src,
                                                                   int src_logb) {
-  constexpr int PITCHED = NTT_ELEMS + NTT_ELEMS / 16;
+  constexpr int PITCHED = ELEMS + ELEMS / 16;
   __shared__ uint4 bufA[PITCHED];     // limbs 0..3 (16-byte accesses, as the canonical kernel)
   __shared__ uint32_t bufB[PITCHED];  // limb 4
   const int R = 1 << r;
-  const int G = NTT_ELEMS >> r;
+  const int G = ELEMS >> r;
   const size_t S = (size_t)1 << logS;
   const int log_gpc = logN - r;
   const size_t gpc = (size_t)1 << log_gpc;
@@ -863,7 +951,7 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
     return (col << logN) + ((Hb << logS) << r) + (size_t)t * S + L;
   };
   const size_t Nmask = ((size_t)1 << logN) - 1;
-  for (int e = threadIdx.x; e < NTT_ELEMS; e += NTT_THREADS) {
+  for (int e = threadIdx.x; e < ELEMS; e += NTT_THREADS) {
     const int g = gfast ? (e % G) : (e >> r);
     const int t = gfast ? (e / G) : (e & (R - 1));
     bool ok;
@@ -903,7 +991,7 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
   // group; stage lh pairs (0,1), (2,3) under one twiddle, stage lh+1 pairs (0,2), (1,3)
   for (; lh + 1 < r; lh += 2) {
     const int h = 1 << lh;
-    constexpr int QPT = NTT_ELEMS / 4 / NTT_THREADS;
+    constexpr int QPT = ELEMS / 4 / NTT_THREADS;
 #pragma unroll
     for (int i = 0; i < QPT; i++) {
       const int u = threadIdx.x + NTT_THREADS * i;
@@ -930,7 +1018,7 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
   }
   if (lh < r) {  // odd stage count: one radix-2 stage
     const int h = 1 << lh;
-    constexpr int BPT = NTT_ELEMS / 2 / NTT_THREADS;
+    constexpr int BPT = ELEMS / 2 / NTT_THREADS;
 #pragma unroll
     for (int i = 0; i < BPT; i++) {
       const int u = threadIdx.x + NTT_THREADS * i;
@@ -949,7 +1037,7 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
     }
     __syncthreads();
   }
-  for (int e = threadIdx.x; e < NTT_ELEMS; e += NTT_THREADS) {
+  for (int e = threadIdx.x; e < ELEMS; e += NTT_THREADS) {
     const int g = gfast ? (e % G) : (e >> r);
     const int t = gfast ? (e / G) : (e & (R - 1));
     bool ok;
@@ -1029,10 +1117,16 @@ static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
     for (const int r : rs) {
       size_t groups = (N >> r) * ncols;
       size_t G = NTT_ELEMS >> r;
-      if (ntt_lazy_enabled())
-        ntt_dit_lazy_kernel<<<(unsigned)((groups + G - 1) / G), NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots,
-                                                                                    cur == lo ? src : nullptr, src_logb);
-      else
+      if (ntt_lazy_enabled()) {
+        const bool wide = G < 8 && ((size_t)1 << cur) >= G;  // see ntt_dit_lazy_kernel
+        const size_t Gw = wide ? 2 * G : G;
+        const unsigned grid = (unsigned)((groups + Gw - 1) / Gw);
+        const fe* sp = cur == lo ? src : nullptr;
+        if (wide)
+          ntt_dit_lazy_kernel<2 * NTT_ELEMS><<<grid, NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots, sp, src_logb);
+        else
+          ntt_dit_lazy_kernel<NTT_ELEMS><<<grid, NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots, sp, src_logb);
+      } else
         ntt_pass_kernel<false><<<(unsigned)((groups + G - 1) / G), NTT_THREADS, 0, s>>>(
             d, ncols, logN, r, cur, roots, logTab, cur == lo ? src : nullptr, src_logb);
       cur += r;
