@@ -44,6 +44,7 @@ METRIC = "segment-proofs/sec at 65536 rows, blowup=16; proof bytes bit-exact vs 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SEED0 = 0x5EED0001             # segment seed of rank / segment 0
 GOLDEN = os.path.join(ROOT, "tests", "golden", "proof_2p16.json")
+CHAIN = os.path.join(ROOT, "tests", "golden", "chain_2p16.json")  # the multi-segment program (make_chain_goldens.py)
 VALU_MIX = os.path.join(ROOT, "profiles", "r02", "valu_mix.json")
 ROW_KERNEL = {"mfma": "hash_rows_pm_kernel<0>", "lane": "hash_rows_kernel<0>"}
 
@@ -94,6 +95,50 @@ def parity_of(proof, seed, log_n):
     want = golden_sha(seed, log_n)
     got = hashlib.sha256(proof).hexdigest()
     return {"seed": hex(seed), "sha256": got, "golden": "match" if want == got else ("none" if want is None else "MISMATCH")}
+
+
+def chain_table():
+    try:
+        return json.load(open(CHAIN))
+    except (OSError, ValueError):
+        return None
+
+
+def chain_segment(zkl_hip, i, log_n):
+    """Segment i of the synthetic multi-segment program (tests/golden/chain_2p16.json): program
+    seed P, ops seed P + i, ROM lane 0 entering where segment i - 1 ended.  The committed table
+    gives every segment's entry value, so a rank builds only its own segments."""
+    tab = chain_table()
+    if tab is None or log_n != tab["log_n"] or i >= len(tab["rom0_in"]):
+        raise RuntimeError(f"no chain table entry for segment {i} at 2^{log_n} rows (run make_chain_goldens.py)")
+    return zkl_hip.synth_vm_segment_chain(tab["program_seed"], tab["program_seed"] + i, log_n, int(tab["rom0_in"][i], 16))
+
+
+def chain_parity(i, proof):
+    tab = chain_table() or {}
+    want = next((s["sha256"] for s in tab.get("segments", []) if s["index"] == i), None)
+    got = hashlib.sha256(proof).hexdigest()
+    return "match" if want == got else ("none" if want is None else "MISMATCH")
+
+
+def chain_step(zkl_hip, i, total, pi, proof):
+    """zl1 step proof of chain segment i of `total` (VM state hashes state_in = i, state_out = i + 1)."""
+    info = zkl_hip.step_info_for(pi, i, total, i.to_bytes(32, "little"), (i + 1).to_bytes(32, "little"))
+    return zkl_hip.step_proof_encode(pi, info, proof)
+
+
+def aggregate(zkl_hip, steps):
+    """The aggregation proof over the gathered step proofs (zkl_agg_prove: build_public +
+    RecursionBackend::prove + ZKLRC1 encode, lib.rs:295-551), host-side on rank 0."""
+    t0 = time.perf_counter()
+    art, dg = zkl_hip.agg_prove(steps)
+    ms = (time.perf_counter() - t0) * 1e3
+    out = {"children": len(steps), "ms": round(ms, 1), "artifact_bytes": len(art), "recursion_digest": dg.hex(),
+           "field_extension": "quadratic (min_security_bits 128)"}
+    g = (chain_table() or {}).get("aggregation")
+    if g and g["children"] == len(steps):
+        out["golden"] = "match" if g["sha256"] == hashlib.sha256(art).hexdigest() else "MISMATCH"
+    return out
 
 
 def cpu_model():
@@ -245,7 +290,7 @@ class Pipeline:
         self.ctxs = [zkl_hip.Context(device) for _ in range(inflight)]
         self.segs = []
         for k, i in enumerate(seg_ids):
-            t, pi, w = zkl_hip.synth_vm_segment(SEED0 + i, log_n)
+            t, pi, w = chain_segment(zkl_hip, i, log_n)
             c = self.ctxs[k % inflight]
             d = c.alloc(w * self.n * 16)
             c.upload(d, t, w * self.n * 16)
@@ -291,20 +336,22 @@ def step_info(zkl_hip, pi, index, total):
     return info
 
 
-def handoff(zkl_hip, dist, items, total):
+def handoff(zkl_hip, dist, items, total, chained=False):
     """Aggregation hand-off: each rank wraps its proofs as zl1 steps (ZKLSTP1),
     rank 0 gathers, orders and chain-checks them and forms the children root the aggregation
-    proof commits to (agg/child.rs:853-895)."""
+    proof commits to (agg/child.rs:853-895).  Returns (summary, ordered step bytes) on rank 0."""
     t_h = time.perf_counter()
-    steps = dist.collect_step_proofs([zkl_hip.step_proof_encode(pi, step_info(zkl_hip, pi, i, total), proof)
-                                      for i, pi, proof in items])
+    enc = [chain_step(zkl_hip, i, total, pi, proof) if chained else
+           zkl_hip.step_proof_encode(pi, step_info(zkl_hip, pi, i, total), proof) for i, pi, proof in items]
+    steps = dist.collect_step_proofs(enc)
     if steps is None:
-        return None
+        return None, None
     root = zkl_hip.children_root(bytes(steps[0]["program_id"]), [d["digest"] for d in steps],
                                  [d["root_trace"] for d in steps])
-    return {"segments": len(steps), "step_bytes": sum(d["bytes"] for d in steps),
-            "ms": round((time.perf_counter() - t_h) * 1e3, 2), "children_root": root[:16].hex(),
-            "transport": "gloo (host bytes; the proofs already live in host memory)"}
+    return ({"segments": len(steps), "step_bytes": sum(d["bytes"] for d in steps),
+             "ms": round((time.perf_counter() - t_h) * 1e3, 2), "children_root": root[:16].hex(),
+             "transport": "gloo (host bytes; the proofs already live in host memory)"},
+            [d["raw"] for d in steps])
 
 
 def main():
@@ -414,7 +461,7 @@ def main():
         ctx.set_kernel_timing(1)
     ctx.free(d_trace)
     ctx.close()
-    hand = handoff(zkl_hip, dist, [(rank, pi, proof)], world)
+    hand, _ = handoff(zkl_hip, dist, [(rank, pi, proof)], world)
 
     # configs[3] shape: S distinct segments sharded over the ranks, pipelined per rank
     c4 = None
@@ -427,17 +474,21 @@ def main():
         dist.barrier()
         el4 = dist.max_over_ranks(time.perf_counter() - t1)
         items = pl.proofs()
-        par4 = dist.gather_to_root([parity_of(p, SEED0 + i, log_n)["golden"] for i, _, p in items])
+        par4 = dist.gather_to_root([chain_parity(i, p) for i, _, p in items])
         pl.close()
-        h4 = handoff(zkl_hip, dist, items, n_seg)
+        h4, steps4 = handoff(zkl_hip, dist, items, n_seg, chained=True)
         if rank == 0:
             flat = [g for r in par4 for g in r]
-            c4 = {"config": f"BASELINE configs[3] shape: {n_seg} distinct synthetic 2^{log_n}-row segments sharded "
-                            f"over {world} rank(s), {args.inflight} contexts in flight per rank, then the step-proof "
-                            "gather and children root on rank 0",
+            c4 = {"config": f"BASELINE configs[3] shape: a {n_seg}-segment synthetic program (2^{log_n}-row segments, "
+                            f"ROM and VM-state chains) sharded over {world} rank(s), {args.inflight} contexts in flight "
+                            "per rank, then the step-proof gather, children root and aggregation proof on rank 0",
                   "value": round(n_seg / el4, 4), "unit": "segment-proofs/s", "seconds": round(el4, 3),
                   "golden_matches": flat.count("match"), "golden_mismatches": flat.count("MISMATCH"),
                   "handoff": h4}
+            try:
+                c4["aggregation"] = aggregate(zkl_hip, steps4)
+            except Exception as e:  # reported, never fatal for the headline number
+                c4["aggregation"] = {"error": str(e)}
 
     if rank == 0:
         value = world * args.steps / elapsed
@@ -513,15 +564,21 @@ def main():
                     dt = time.perf_counter() - t1
                     best = dt if best is None else min(best, dt)
                 if k == max(int(x) for x in args.c3_inflight.split(",") if x):
-                    g = [parity_of(p, SEED0 + i, log_n)["golden"] for i, _, p in pl.proofs()]
+                    g = [chain_parity(i, p) for i, _, p in pl.proofs()]
                     c3_par = {"golden_matches": g.count("match"), "golden_mismatches": g.count("MISMATCH")}
+                    c3_steps = [chain_step(zkl_hip, i, args.c3_segments, spi, p) for i, spi, p in pl.proofs()]
                 pl.close()
                 c3[str(k)] = round(args.c3_segments / best, 4)
             kbest = max(c3, key=lambda k: c3[k])
             out["c3_in_gpu_pipeline"] = {
-                "config": f"BASELINE configs[2] shape: {args.c3_segments} distinct synthetic 2^{log_n}-row segments on 1 GPU",
+                "config": f"BASELINE configs[2] shape: the first {args.c3_segments} segments of a synthetic "
+                          f"multi-segment program (2^{log_n} rows each) on 1 GPU",
                 "segment_proofs_per_s_by_inflight": c3, "best_inflight": int(kbest), "value": c3[kbest],
                 "unit": "segment-proofs/s", "parity": c3_par}
+            try:
+                out["c3_in_gpu_pipeline"]["aggregation"] = aggregate(zkl_hip, c3_steps)
+            except Exception as e:  # reported, never fatal for the headline number
+                out["c3_in_gpu_pipeline"]["aggregation"] = {"error": str(e)}
         if world == 1 and args.c5_log_n > 0:
             try:
                 ms5, pb5 = c5_single(zkl_hip, device, args.c5_log_n)

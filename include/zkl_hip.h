@@ -257,6 +257,12 @@ int zkl_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128* trace_out,
 #define ZKL_SYN_MERKLE 4u
 int zkl_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f128* trace_out,
                             zkl_air_public_inputs* pi_out, uint32_t* width_out);
+/* Same with the program identity taken from program_seed (the ops still from seed) and ROM
+ * lane 0 entering the first level at *rom0_in (NULL: 0), so that consecutive synthetic
+ * segments are segments of one program and form the accumulator chain the aggregation checks
+ * (agg/trace.rs:524-541: rom_s_in[0] of segment i+1 == rom_s_out[0] of segment i). */
+int zkl_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t log_n, uint32_t flags, const zkl_f128* rom0_in,
+                               zkl_f128* trace_out, zkl_air_public_inputs* pi_out, uint32_t* width_out);
 
 /* ---- zl1 step proof (host-side, no device work) ----------------------------------
  * StepProof::to_bytes (proof/step.rs:79-151) of the step proof prove_segment builds around
@@ -278,6 +284,34 @@ int zkl_step_proof_digest(const uint8_t* step, size_t len, uint8_t digest_out[32
  * a multi-GPU run computes it after gathering the step proofs. */
 int zkl_children_root(const uint8_t suite_id[32], const uint8_t* digests, const uint8_t* root_traces, uint32_t n,
                       uint8_t root_out[32]);
+
+/* ---- aggregation proof -------------------------------------
+ * zk_lisp_proof::ProverOptions as the aggregation reads it (zk-lisp-proof/src/lib.rs:40-66). */
+typedef struct {
+  uint32_t queries;           /* the aggregation proves with max(queries, 16) (prove.rs:645) */
+  uint32_t blowup;
+  uint32_t grind;
+  uint32_t min_security_bits; /* >= 128: FieldExtension::Quadratic, else None (prove.rs:647-651);
+                                 >= 64: conjectured-security check (prove.rs:664-681) */
+} zkl_agg_options;
+
+/* What `zk-lisp prove` does after the segment proofs (replaces the Rust calls
+ * RecursionPublicBuilder::build_public lib.rs:404-482, RecursionBackend::prove lib.rs:295-344
+ * -> prove_agg_proof prove.rs:629-719, RecursionArtifactCodec::encode lib.rs:486-551):
+ * n ZKLSTP1 step proofs in, the ZKLRC1 artifact (the aggregation proof inside) out, plus the
+ * recursion digest (recursion_digest_from_agg_pi, prove.rs:585-616) when digest_out != NULL.
+ * Each child's Fiat-Shamir transcript is replayed from its step proof alone (agg/fs.rs:38-245)
+ * and every opening, DEEP value, FRI fold, remainder and PoW is checked; a child that fails
+ * is rejected (ZKL_E_INVALID) rather than aggregated into an unsatisfiable trace.  The
+ * artifact is freed with zkl_hip_free.  Host-only (no ctx, no device). */
+int zkl_agg_prove(const uint8_t* const* steps, const size_t* step_lens, uint32_t n_steps,
+                  const zkl_agg_options* opts, uint8_t** artifact_out, size_t* artifact_len,
+                  uint8_t digest_out[32]);
+/* The aggregation trace of the same batch (build_agg_trace_from_transcripts,
+ * agg/trace.rs:155-238): 31 columns x rows, column-major; rows_out receives the row count
+ * (a power of two >= 8); out may be NULL to query it. */
+int zkl_agg_trace(const uint8_t* const* steps, const size_t* step_lens, uint32_t n_steps,
+                  zkl_f128* out, uint32_t max_rows, uint32_t* rows_out);
 
 #ifdef __cplusplus
 }

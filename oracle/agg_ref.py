@@ -1,0 +1,793 @@
+"""Aggregation proof, CPU restatement -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/ load this module (as the checker of the library's zkl_agg_prove / zkl_agg_trace);
+nothing in the product path imports it.  It restates, over Python integers, what the
+reference's `zk-lisp prove` does after the segment proofs exist:
+
+  StepProof::from_bytes                         proof/step.rs:153-493
+  ZlChildTranscript::from_step / FS replay      agg/child.rs:597-848, agg/fs.rs:38-245
+  RecursionPublicBuilder::build_public          lib.rs:404-482
+  AggAirPublicInputs::to_elements               agg/pi.rs:174-218
+  build_agg_trace_from_transcripts              agg/trace.rs:95-238, 250-693, 697-1685
+  ZlAggAir                                      agg/air.rs:31-332
+  prove_agg_proof (Quadratic at >= 128 bits)    prove.rs:629-719  -> winterfell 0.13.1 Prover [WF-recall]
+  recursion_digest_from_agg_pi                  prove.rs:585-616
+  RecursionArtifactCodec::encode                lib.rs:486-551
+
+Poseidon (sponge, merge, merge_with_int), BLAKE3, roots of unity, the step digest and the
+children root come from the C oracle through `ol` (tests/oracle_lib.py), which the oracle
+tests pin separately.  Everything else -- f128 and QuadExtension<f128> arithmetic, NTTs, the
+AIR, the prover and the byte formats -- is written out here.  Parity is unpinned in the sense
+of DESIGN.md §3: the reference holds no aggregation fixtures.
+"""
+import struct
+
+P = 2 ** 128 - 45 * 2 ** 40 + 1
+GEN = 3  # BaseElement::GENERATOR, the domain offset
+
+
+def inv(a):
+    return pow(a % P, P - 2, P)
+
+
+# ---- QuadExtension<f128>: a + b*phi, phi^2 = phi - 1 (winter-math f128 ExtensibleField<2>) ----
+def qmul(x, y):
+    a0, a1 = x
+    b0, b1 = y
+    z = a0 * b0 % P
+    return ((z - a1 * b1) % P, ((a0 + a1) * (b0 + b1) - z) % P)
+
+
+def qadd(x, y):
+    return ((x[0] + y[0]) % P, (x[1] + y[1]) % P)
+
+
+def qsub(x, y):
+    return ((x[0] - y[0]) % P, (x[1] - y[1]) % P)
+
+
+def qscale(x, s):
+    return (x[0] * s % P, x[1] * s % P)
+
+
+def qinv(x):
+    a, b = x
+    n = (a * a + a * b + b * b) % P
+    ni = inv(n)
+    return ((a + b) * ni % P, (-b) * ni % P)
+
+
+class Field:
+    """Arithmetic of the proof's E: the base field (ext 1) or the quadratic extension (ext 2);
+    values are ints or (a, b) tuples."""
+
+    def __init__(self, ext):
+        self.ext = ext
+
+    def lift(self, v):
+        return (v % P, 0) if self.ext == 2 else v % P
+
+    def add(self, x, y):
+        return qadd(x, y) if self.ext == 2 else (x + y) % P
+
+    def sub(self, x, y):
+        return qsub(x, y) if self.ext == 2 else (x - y) % P
+
+    def mul(self, x, y):
+        return qmul(x, y) if self.ext == 2 else x * y % P
+
+    def scale(self, x, s):
+        return qscale(x, s) if self.ext == 2 else x * s % P
+
+    def inv(self, x):
+        return qinv(x) if self.ext == 2 else inv(x)
+
+    def zero(self):
+        return self.lift(0)
+
+    def is_zero(self, x):
+        return x == self.zero()
+
+    def flat(self, x):  # E::as_base_elements
+        return list(x) if self.ext == 2 else [x]
+
+    def draw(self, coin):  # RandomCoin::draw::<E>: digest bytes [value | 16 zero bytes]
+        v = coin.draw()
+        return (v, 0) if self.ext == 2 else v
+
+
+# ---- hashing / transcript ---------------------------------------------------------------
+class Coin:
+    """DefaultRandomCoin<PoseidonHasher> [WF-recall]; the transcript order is agg/fs.rs:67-237."""
+
+    def __init__(self, ol, elems):
+        self.ol = ol
+        self.seed = ol.hash_elements(elems)
+        self.ctr = 0
+
+    def reseed(self, d):
+        self.seed = self.ol.merge(self.seed, d)
+        self.ctr = 0
+
+    def draw(self):
+        self.ctr += 1
+        return self.ol.merge_with_int(self.seed, self.ctr)
+
+
+def merkle(ol, leaves):
+    n = len(leaves)
+    t = [0] * n + list(leaves)
+    for i in range(n - 1, 0, -1):
+        t[i] = ol.merge(t[2 * i], t[2 * i + 1])
+    return t
+
+
+# ---- byte reading / writing -----------------------------------------------------------------
+class W:
+    def __init__(self):
+        self.b = bytearray()
+
+    def u8(self, x):
+        self.b += bytes([x])
+
+    def u16(self, x):
+        self.b += struct.pack("<H", x)
+
+    def u32(self, x):
+        self.b += struct.pack("<I", x)
+
+    def u64(self, x):
+        self.b += struct.pack("<Q", x)
+
+    def raw(self, x):
+        self.b += bytes(x)
+
+    def usize(self, x):  # winter-utils write_usize (vint64)
+        if x < 2 ** 56:
+            ln = max(1, (x.bit_length() + 6) // 7)
+            self.b += ((x << 1 | 1) << (ln - 1)).to_bytes(ln, "little")
+        else:
+            self.b += b"\x00" + struct.pack("<Q", x)
+
+    def fe(self, x):
+        self.b += (x % P).to_bytes(16, "little")
+
+    def digest(self, x):
+        self.b += (x % P).to_bytes(16, "little") + bytes(16)
+
+    def vec(self, w):
+        self.usize(len(w.b))
+        self.b += w.b
+
+
+class R:
+    def __init__(self, b):
+        self.b, self.o = bytes(b), 0
+
+    def take(self, k):
+        if self.o + k > len(self.b):
+            raise ValueError("truncated")
+        self.o += k
+        return self.b[self.o - k:self.o]
+
+    def u8(self):
+        return self.take(1)[0]
+
+    def u32(self):
+        return struct.unpack("<I", self.take(4))[0]
+
+    def u64(self):
+        return struct.unpack("<Q", self.take(8))[0]
+
+    def usize(self):
+        first = self.b[self.o]
+        if first == 0:
+            self.o += 1
+            return self.u64()
+        ln = (first & -first).bit_length()
+        return int.from_bytes(self.take(ln), "little") >> ln
+
+    def fe(self):
+        v = int.from_bytes(self.take(16), "little")
+        if v >= P:
+            raise ValueError("non-canonical element")
+        return v
+
+    def digest(self):
+        v = self.fe()
+        if self.take(16) != bytes(16):
+            raise ValueError("digest upper half must be zero")
+        return v
+
+    def vec(self):
+        return R(self.take(self.usize()))
+
+
+def le16(b):
+    return int.from_bytes(bytes(b[:16]), "little") % P
+
+
+def fold32(b):  # fold_bytes32_to_fe (utils.rs:359-371)
+    return (le16(b[:16]) + le16(b[16:32]) * 2 ** 64) % P
+
+
+# ---- step proofs and child transcripts ----------------------------------------------------
+def decode_step(ol, b):
+    """StepProof::from_bytes (step.rs:153-493) + StepMeta::from_env (step.rs:516-533)."""
+    r = R(b)
+    assert r.take(7) == b"ZKLSTP1"
+    s = {"lambda_bits": r.u32(), "suite": r.take(32), "program_id": r.take(32), "program_commitment": r.take(32),
+         "merkle_root": r.take(32), "feature_mask": r.u64()}
+    args = []
+    for _ in range(r.u32()):
+        tag = r.u8()
+        args.append((tag, r.take({0: 8, 1: 16, 2: 32}[tag])))
+    s["main_args"] = args
+    s["vm_usage_mask"], s["ram_delta_clk_bits"] = r.u32(), r.u32()
+    s["rom_acc"] = [le16(r.take(32)) for _ in range(3)]
+    s["segment_index"], s["segments_total"] = r.u32(), r.u32()
+    s["pc_init"] = r.take(32)
+    s["bnd"] = [r.take(32) for _ in range(12)]
+    s["inner"] = r.take(r.u32())
+    if s["segments_total"] <= 1:
+        s["segment_index"], s["segments_total"] = 0, 1
+    inner = s["inner"]
+    logn, blowup, q = inner[3], inner[6 + 1 + 16 + 1], inner[6 + 1 + 16]
+    slots = sum(2 if t == 2 else 1 for t, _ in args)
+    s.update(m=1 << logn, rho=blowup, q=q, o=2, lam=min(s["lambda_bits"], 65535), pi_len=5 + slots + 13)
+    s["v_units"] = s["m"] * s["q"]
+    s["digest"], s["root_trace"] = ol.step_digest(bytes(b))
+    return s
+
+
+def replay_pi_elements(ol, s):
+    """AirPublicInputs::to_elements (lib.rs:116-160) of the inputs agg/fs.rs:44-65 rebuilds."""
+    out = [s["feature_mask"], le16(s["program_commitment"]), le16(s["merkle_root"])]
+    if any(s["program_commitment"]):
+        out += list(ol.program_field_commitment(bytes(s["program_commitment"])))
+    else:
+        out += [0, 0]
+    for tag, v in s["main_args"]:  # encode_vmarg_to_elements (utils.rs:79-97)
+        if tag == 0:
+            out.append(int.from_bytes(v, "little"))
+        elif tag == 1:
+            out.append(int.from_bytes(v, "little") % P)
+        else:
+            out += [le16(v[:16]), le16(v[16:])]
+    out.append(le16(s["pc_init"]))
+    out += [le16(s["bnd"][k]) for k in range(2, 12)]
+    out += [s["vm_usage_mask"], s["ram_delta_clk_bits"]]
+    return out
+
+
+def context_elements(W, n, q, blowup, grind, ext, fold=2, rem=1):
+    """Context::to_elements [WF-recall]: TraceInfo, field modulus halves, packed options."""
+    return [W << 8, n, P & (2 ** 64 - 1), P >> 64, (ext << 16) | (fold << 8) | rem, grind, blowup, q]
+
+
+def child_transcript(ol, s):
+    """Parse the inner proof and replay its transcript (agg/fs.rs:38-245, agg/child.rs:597-848)."""
+    r = R(s["inner"])
+    W = r.u8()
+    r.take(2)
+    logn = r.u8()
+    r.take(2)
+    assert r.u8() == 16
+    r.take(16)
+    q, blowup, grind, ext, fold, rem_deg = (r.u8() for _ in range(6))
+    r.take(4)
+    nq = r.u8()
+    n, N = 1 << logn, (1 << logn) * blowup
+    rem_max = (rem_deg + 1) * blowup
+    nl, d = 0, N
+    while d > rem_max:
+        nl, d = nl + 1, d // 2
+    cm = r.vec()
+    troot, croot = cm.digest(), cm.digest()
+    fri_roots = [cm.digest() for _ in range(nl)]
+    rem_commit = cm.digest()
+    assert r.usize() == 1
+    tq_v, _tq_p, cq_v, _cq_p, ood_ts, ood_es = (r.vec() for _ in range(6))
+    C = len(cq_v.b) // (nq * 16)  # constraint frame width from the bytes (agg/child.rs:299-340)
+    layers = []
+    assert r.usize() == nl
+    for _ in range(nl):
+        lv, _lp = r.vec(), r.vec()
+        vals = [lv.fe() for _ in range(len(lv.b) // 16)]
+        layers.append([(vals[2 * k], vals[2 * k + 1]) for k in range(len(vals) // 2)])
+    rv = r.vec()
+    remainder = [rv.fe() for _ in range(len(rv.b) // 16)]
+    r.u8()
+    nonce = r.u64()
+
+    coin = Coin(ol, context_elements(W, n, q, blowup, grind, ext) + replay_pi_elements(ol, s))
+    coin.reseed(troot)
+    coin.reseed(croot)
+    z = coin.draw()
+    tz = [ood_ts.fe() for _ in range(W)]
+    tzg = [ood_ts.fe() for _ in range(W)]
+    hz = [ood_es.fe() for _ in range(C)]
+    hzg = [ood_es.fe() for _ in range(C)]
+    coin.reseed(ol.hash_elements(tz + hz + tzg + hzg))
+    deep = [coin.draw() for _ in range(W + C)]
+    alphas = []
+    for root in fri_roots + [rem_commit]:
+        coin.reseed(root)
+        alphas.append(coin.draw())
+    tzeros = ol.merge_with_int(coin.seed, nonce) & (2 ** 64 - 1)
+    assert tzeros and (tzeros & -tzeros).bit_length() - 1 >= grind or grind == 0
+    coin.seed, coin.ctr = ol.merge_with_int(coin.seed, nonce), 0
+    positions = sorted(set(coin.draw() & (N - 1) for _ in range(q)))
+    assert len(positions) == nq
+    trows = [[tq_v.fe() for _ in range(W)] for _ in range(nq)]
+    crows = [[cq_v.fe() for _ in range(C)] for _ in range(nq)]
+    return dict(W=W, C=C, n=n, N=N, z=z, tz=tz, tzg=tzg, hz=hz, hzg=hzg, deep=deep, alphas=alphas[:nl],
+                positions=positions, trows=trows, crows=crows, layers=layers, remainder=remainder)
+
+
+# ---- aggregation public inputs, trace ----------------------------------------------------
+def build_public(ol, steps):
+    """RecursionPublicBuilder::build_public (lib.rs:404-482)."""
+    f, l = steps[0], steps[-1]
+    h = W()
+    h.raw(b"zkl/pi/v1")
+    h.raw(f["program_id"])
+    h.raw(f["program_commitment"])
+    h.raw(f["merkle_root"])
+    h.u64(f["feature_mask"])
+    h.u32(len(f["main_args"]))
+    for tag, v in f["main_args"]:
+        h.u8(tag)
+        h.raw(v)
+    return dict(program_id=f["program_id"], program_commitment=f["program_commitment"], pi_digest=ol.blake3(bytes(h.b)),
+                children_root=ol.children_root(f["suite"], [s["digest"] for s in steps], [s["root_trace"] for s in steps]),
+                batch_id=bytes(32), v_units_total=sum(s["v_units"] for s in steps), children_count=len(steps),
+                m=f["m"], rho=f["rho"], q=f["q"], o=f["o"], lam=f["lam"], pi_len=f["pi_len"], v_units=f["v_units"],
+                lde_blowup=f["rho"], folding=2, redundancy=1, num_layers=1, num_queries=f["q"], grinding=0,
+                suite=f["suite"], children_ms=[s["m"] for s in steps], vm0=f["bnd"][0], vm1=l["bnd"][1],
+                ru0=f["bnd"][2], ru1=l["bnd"][3], rs0=f["bnd"][4], rs1=l["bnd"][5], rom0=f["bnd"][6:9],
+                rom1=l["bnd"][9:12])
+
+
+def agg_pi_elements(p):
+    """AggAirPublicInputs::to_elements (agg/pi.rs:174-218)."""
+    out = [fold32(p[k]) for k in ("program_id", "program_commitment", "pi_digest", "children_root", "batch_id")]
+    out += [p[k] for k in ("m", "rho", "q", "o", "lam", "pi_len", "v_units", "lde_blowup", "folding", "redundancy",
+                           "num_layers", "num_queries", "grinding", "children_count", "v_units_total")]
+    out += [fold32(p[k]) for k in ("vm0", "vm1", "ru0", "ru1", "rs0", "rs1")]
+    out += [fold32(x) for x in p["rom0"]] + [fold32(x) for x in p["rom1"]]
+    return out
+
+
+def _fold_positions(pos, size):  # fold_positions_usize (agg/child.rs:1072-1100)
+    out = []
+    for x in pos:
+        y = x % (size // 2)
+        if y not in out:
+            out.append(y)
+    return out
+
+
+def _xs(ol, y, size):
+    xe = pow(ol.root_of_unity(size.bit_length() - 1), y, P) * GEN % P
+    return xe, (-xe) % P
+
+
+def _fold(v0, v1, alpha, x0, x1):  # (x1 - x0) vnext = v1 (alpha - x0) - v0 (alpha - x1)
+    return (v1 * (alpha - x0) - v0 * (alpha - x1)) * inv(x1 - x0) % P
+
+
+def _layer_positions(t):
+    out, pos, size = [], t["positions"], t["N"]
+    for _ in t["layers"]:
+        pos = _fold_positions(pos, size)
+        out.append(pos)
+        size //= 2
+    return out
+
+
+def _query_value(t, fpos, d, p, size):  # get_query_values geometry
+    h = size // 2
+    k = fpos[d].index(p % h)
+    return t["layers"][d][k][p // h]
+
+
+def _deep_agg(ol, t, fpos, beta):  # agg/trace.rs:1126-1257
+    g = ol.root_of_unity(t["n"].bit_length() - 1)
+    zg = t["z"] * g % P
+    wN = ol.root_of_unity(t["N"].bit_length() - 1)
+    acc, bp = 0, 1
+    for k, p in enumerate(t["positions"]):
+        x = pow(wN, p, P) * GEN % P
+        iz, izg = inv(x - t["z"]), inv(x - zg)
+        y = 0
+        for i, tx in enumerate(t["trows"][k]):
+            y += t["deep"][i] * ((tx - t["tz"][i]) * iz + (tx - t["tzg"][i]) * izg)
+        for j, cx in enumerate(t["crows"][k]):
+            y += t["deep"][t["W"] + j] * ((cx - t["hz"][j]) * iz + (cx - t["hzg"][j]) * izg)
+        acc = (acc + bp * (y - _query_value(t, fpos, 0, p, t["N"]))) % P
+        bp = bp * beta % P
+    return acc
+
+
+def _fri_layer1_agg(ol, t, fpos, beta):  # agg/trace.rs:1261-1432
+    acc, bp = 0, 1
+    f0 = fpos[0]
+    for k in range(min(len(f0), len(t["positions"]))):
+        x0, x1 = _xs(ol, f0[k], t["N"])
+        v0, v1 = t["layers"][0][k]
+        vn = _fold(v0, v1, t["alphas"][0], x0, x1)
+        acc = (acc + bp * (vn - _query_value(t, fpos, 1, f0[k], t["N"] // 2))) % P
+        bp = bp * beta % P
+    return acc
+
+
+def _fri_path_agg(ol, t, fpos, delta, s):  # agg/trace.rs:697-951
+    acc, dp, size = 0, 1, t["N"]
+    nl = len(t["layers"])
+    for d in range(nl):
+        x0, x1 = _xs(ol, fpos[d][s], size)
+        v0, v1 = t["layers"][d][s]
+        vn = _fold(v0, v1, t["alphas"][d], x0, x1)
+        if d + 1 < nl:
+            acc = (acc + dp * (vn - _query_value(t, fpos, d + 1, fpos[d][s], size // 2))) % P
+            dp = dp * delta % P
+        else:
+            v_rem, pos_rem = vn, fpos[d][s]
+        size //= 2
+    xl = GEN * pow(ol.root_of_unity(size.bit_length() - 1), pos_rem, P) % P
+    rv = 0
+    for c in t["remainder"]:
+        rv = (rv * xl + c) % P
+    return (acc + dp * (v_rem - rv)) % P
+
+
+def _fri_paths_agg(ol, t, fpos, delta, beta):
+    acc, bp = 0, 1
+    for k in range(min(len(f) for f in fpos)):
+        acc = (acc + bp * _fri_path_agg(ol, t, fpos, delta, k)) % P
+        bp = bp * beta % P
+    return acc
+
+
+NCOLS = 31
+(OK, V0S, V1S, VNS, FV0, FV1, FVN, FAL, FX0, FX1, FQ1, COMP, ADZ, ML0, FLL, CR, CA, CB, CG, SEG, TRE, CRE, VACC, VCH,
+ CNT, VMERR, RUERR, RSERR, RO0, RO1, RO2) = range(NCOLS)
+
+
+def agg_trace(ol, p, steps, txs):
+    """build_agg_trace_from_transcripts (agg/trace.rs:155-693) for an honest batch: every
+    opening of every child reproduces its commitment (the root errors are zero)."""
+    nc = len(steps)
+    rows = 8
+    while rows < nc:
+        rows *= 2
+    T = [[0] * rows for _ in range(NCOLS)]
+    wc = Coin(ol, agg_pi_elements(p) + [0xA9])  # derive_agg_fs_weights (agg/trace.rs:95-125)
+    beta_deep, beta_l1, delta, beta_paths = (wc.draw() for _ in range(4))
+    v_acc = cnt = 0
+    prev = None
+    for i, (s, t) in enumerate(zip(steps, txs)):
+        ins = [fold32(s["bnd"][k]) for k in (0, 2, 4, 6)]
+        outs = [fold32(s["bnd"][k]) for k in (1, 3, 5, 9)]
+        base = [fold32(p["vm0"]), fold32(p["ru0"]), fold32(p["rs0"]), fold32(p["rom0"][0])]
+        fin = [fold32(p["vm1"]), fold32(p["ru1"]), fold32(p["rs1"]), fold32(p["rom1"][0])]
+        errs = [(ins[k] - (prev[k] if prev else base[k])) % P for k in range(4)]
+        if i + 1 == nc:
+            errs = [(errs[k] + outs[k] - fin[k]) % P for k in range(4)]
+        T[SEG][i], T[VCH][i], T[VACC][i], T[CNT][i] = 1, s["v_units"], v_acc, cnt
+        T[VMERR][i], T[RUERR][i], T[RSERR][i], T[RO0][i] = errs
+        fpos = _layer_positions(t)
+        x0, x1 = _xs(ol, fpos[0][0], t["N"])
+        v0, v1 = t["layers"][0][0]
+        vn = _fold(v0, v1, t["alphas"][0], x0, x1)
+        T[FV0][i], T[FV1][i], T[FVN][i], T[FAL][i], T[FX0][i], T[FX1][i] = v0, v1, vn, t["alphas"][0], x0, x1
+        T[FQ1][i] = _query_value(t, fpos, 1, fpos[0][0], t["N"] // 2)
+        T[COMP][i] = _deep_agg(ol, t, fpos, beta_deep)
+        T[ADZ][i] = _fri_layer1_agg(ol, t, fpos, beta_l1)
+        T[ML0][i] = _fri_path_agg(ol, t, fpos, delta, 0)
+        T[FLL][i] = _fri_paths_agg(ol, t, fpos, delta, beta_paths)
+        v_acc += s["v_units"]
+        cnt += 1
+        prev = outs
+    for r in range(nc, rows):
+        T[VACC][r], T[CNT][r] = v_acc, cnt
+    return T
+
+
+# ---- ZlAggAir and the winterfell prover -----------------------------------------------------
+def agg_transition(c, x, is_last):  # agg/air.rs:113-274
+    nl = (1 - is_last) % P
+    r = [c[OK], nl * (x[VACC] - (c[VACC] + c[VCH] * c[SEG])), c[TRE], c[CRE]]
+    r += [nl * (x[k] - c[k]) for k in (CR, CA, CB, CG, V0S, V1S, VNS)]
+    r.append(nl * (x[CNT] - (c[CNT] + c[SEG])))
+    r.append(c[FVN] * (c[FX1] - c[FX0]) - (c[FV1] * (c[FAL] - c[FX0]) - c[FV0] * (c[FAL] - c[FX1])))
+    r.append(c[FVN] - c[FQ1])
+    r += [c[k] for k in (COMP, ADZ, ML0, FLL, VMERR, RUERR, RSERR, RO0, RO1, RO2)]
+    return [v % P for v in r]
+
+
+DEGREES = [(1, 0), (2, 1)] + [(1, 0)] * 9 + [(1, 1)] + [(1, 0)] * 12  # (base, #cycles of period n)
+
+
+def _ntt(ol, a, inverse, F):
+    m = len(a)
+    a = list(a)
+    j = 0
+    for i in range(1, m):
+        bit = m >> 1
+        while j & bit:
+            j ^= bit
+            bit >>= 1
+        j |= bit
+        if i < j:
+            a[i], a[j] = a[j], a[i]
+    length = 2
+    while length <= m:
+        w = ol.root_of_unity(length.bit_length() - 1)
+        if inverse:
+            w = inv(w)
+        h = length // 2
+        tw = [pow(w, k, P) for k in range(h)]
+        for i in range(0, m, length):
+            for k in range(h):
+                u, v = a[i + k], F.scale(a[i + k + h], tw[k])
+                a[i + k], a[i + k + h] = F.add(u, v), F.sub(u, v)
+        length *= 2
+    if inverse:
+        mi = inv(m)
+        a = [F.scale(x, mi) for x in a]
+    return a
+
+
+def _interp(ol, vals, offset, F):
+    c = _ntt(ol, vals, True, F)
+    oi = inv(offset)
+    return [F.scale(x, pow(oi, k, P)) for k, x in enumerate(c)]
+
+
+def _evaluate(ol, coef, M, offset, F):
+    v = [F.scale(x, pow(offset, k, P)) for k, x in enumerate(coef)] + [F.zero()] * (M - len(coef))
+    return _ntt(ol, v, False, F)
+
+
+def _horner(coef, x, F):
+    acc = F.zero()
+    for c in reversed(coef):
+        acc = F.add(F.mul(acc, x), c)
+    return acc
+
+
+def _multiproof(w, tree, n_leaves, idx):
+    """BatchMerkleProof bytes [WF-recall]: depth, #pairs, per pair its sibling list."""
+    req = sorted(set(idx))
+    pairs = sorted(set(i & ~1 for i in req))
+    lists = [[n_leaves + j for j in (b, b + 1) if j not in req] for b in pairs]
+    cur = [(b + n_leaves) >> 1 for b in pairs]
+    depth = n_leaves.bit_length() - 1
+    for _ in range(1, depth):
+        nxt = []
+        i = 0
+        while i < len(cur):
+            sib = cur[i] ^ 1
+            if i + 1 < len(cur) and cur[i + 1] == sib:
+                i += 1
+            else:
+                lists[i].append(sib)  # the list at this position of the level, as prove_batch does
+            nxt.append(sib >> 1)
+            i += 1
+        cur = nxt
+    w.u8(depth)
+    w.u8(len(lists))
+    for lst in lists:
+        w.u8(len(lst))
+        for node in lst:
+            w.digest(tree[node])
+
+
+def prove_agg(ol, T, p, queries, blowup, grind, ext):
+    """winterfell 0.13.1 Prover::prove for ZlAggAir [WF-recall] (prove.rs:629-719)."""
+    F = Field(ext)
+    Wd, n = len(T), len(T[0])
+    for i in range(n - 1):  # the trace satisfies the AIR (winterfell's debug validation)
+        tc = agg_transition([T[c][i] for c in range(Wd)], [T[c][i + 1] for c in range(Wd)], 0)
+        assert not any(tc), f"aggregation trace does not satisfy ZlAggAir (row {i})"
+    logn = n.bit_length() - 1
+    N = n * blowup
+    parts, rate = 1, 8 if Wd <= 32 else 16  # select_partitions_for_trace (utils.rs:394-409)
+    coin = Coin(ol, context_elements(Wd, n, queries, blowup, grind, ext) + agg_pi_elements(p))
+    g = ol.root_of_unity(logn)
+    gl = pow(g, n - 1, P)
+    B = Field(1)
+    tpoly = [_interp(ol, col, 1, B) for col in T]
+    lde = [_evaluate(ol, c, N, GEN, B) for c in tpoly]
+    ttree = merkle(ol, [ol.hash_elements([lde[c][i] for c in range(Wd)]) for i in range(N)])
+    coin.reseed(ttree[1])
+    alphas = [F.draw(coin) for _ in range(24)]
+    betas = [F.draw(coin) for _ in range(5)]
+    last = n - 1
+    asr = [(OK, 0, 0), (VACC, 0, 0), (CNT, 0, 0), (VACC, last, p["v_units_total"]), (CNT, last, p["children_count"])]
+    max_eval = max(b * (n - 1) + c * (n - 1) for b, c in DEGREES)
+    ceb = max(2, max(1 << max(0, (b + c - 1 - 1).bit_length()) for b, c in DEGREES))
+    Cc = max(1, -(-(max_eval - (n - 1)) // n))
+    ce = n * ceb
+    wce = ol.root_of_unity(ce.bit_length() - 1)
+    cev = []
+    for i in range(ce):
+        x = GEN * pow(wce, i, P) % P
+        r0 = i * (N // ce)
+        cur = [lde[c][r0] for c in range(Wd)]
+        nxt = [lde[c][(r0 + blowup) % N] for c in range(Wd)]
+        xn = pow(x, n, P)
+        p_last = gl * (xn - 1) * inv(n * (x - gl)) % P
+        tc = agg_transition(cur, nxt, p_last)
+        t = F.zero()
+        for a, v in zip(alphas, tc):
+            t = F.add(t, F.scale(a, v))
+        t = F.scale(t, (x - gl) * inv(xn - 1) % P)
+        for (col, step, val), b in zip(asr, betas):
+            t = F.add(t, F.scale(b, (cur[col] - val) * inv(x - pow(g, step, P)) % P))
+        cev.append(t)
+    cco = _interp(ol, cev, GEN, F)
+    assert all(F.is_zero(x) for x in cco[Cc * n:]), "aggregation trace does not satisfy ZlAggAir"
+    hpoly = [cco[j * n:(j + 1) * n] for j in range(Cc)]
+    clde = [_evaluate(ol, h, N, GEN, F) for h in hpoly]
+    ctree = merkle(ol, [ol.hash_elements(sum((F.flat(clde[j][i]) for j in range(Cc)), [])) for i in range(N)])
+    coin.reseed(ctree[1])
+    z = F.draw(coin)
+    zg = F.scale(z, g)
+    tz = [_horner([F.lift(c) for c in tp], z, F) for tp in tpoly]
+    tzg = [_horner([F.lift(c) for c in tp], zg, F) for tp in tpoly]
+    hz = [_horner(h, z, F) for h in hpoly]
+    hzg = [_horner(h, zg, F) for h in hpoly]
+    coin.reseed(ol.hash_elements(sum((F.flat(v) for v in tz + hz + tzg + hzg), [])))
+    gam = [F.draw(coin) for _ in range(Wd + Cc)]
+    wN = ol.root_of_unity(N.bit_length() - 1)
+    ev = []
+    for i in range(N):
+        x = F.lift(GEN * pow(wN, i, P))
+        iz, izg = F.inv(F.sub(x, z)), F.inv(F.sub(x, zg))
+        y = F.zero()
+        for c in range(Wd):
+            tv = F.lift(lde[c][i])
+            y = F.add(y, F.mul(gam[c], F.add(F.mul(F.sub(tv, tz[c]), iz), F.mul(F.sub(tv, tzg[c]), izg))))
+        for j in range(Cc):
+            hv = clde[j][i]
+            y = F.add(y, F.mul(gam[Wd + j], F.add(F.mul(F.sub(hv, hz[j]), iz), F.mul(F.sub(hv, hzg[j]), izg))))
+        ev.append(y)
+    layers, trees, roots = [], [], []
+    while len(ev) > 2 * blowup:
+        Nd, h = len(ev), len(ev) // 2
+        tree = merkle(ol, [ol.hash_elements(F.flat(ev[i]) + F.flat(ev[i + h])) for i in range(h)])
+        trees.append(tree)
+        roots.append(tree[1])
+        coin.reseed(tree[1])
+        a = F.draw(coin)
+        wd = ol.root_of_unity(Nd.bit_length() - 1)
+        nx = []
+        for i in range(h):
+            x0 = GEN * pow(wd, i, P) % P
+            x1 = (-x0) % P
+            num = F.sub(F.mul(ev[i + h], F.sub(a, F.lift(x0))), F.mul(ev[i], F.sub(a, F.lift(x1))))
+            nx.append(F.scale(num, inv(x1 - x0)))
+        layers.append(ev)
+        ev = nx
+    rco = _interp(ol, ev, GEN, F)
+    assert all(F.is_zero(x) for x in rco[2:])
+    rem = [rco[1], rco[0]]
+    rem_commit = ol.hash_elements(F.flat(rem[0]) + F.flat(rem[1]))
+    coin.reseed(rem_commit)
+    nonce = 1
+    if grind:
+        nonce = 1
+        while True:
+            v = ol.merge_with_int(coin.seed, nonce) & (2 ** 64 - 1)
+            if v and (v & -v).bit_length() - 1 >= grind:
+                break
+            nonce += 1
+    coin.seed, coin.ctr = ol.merge_with_int(coin.seed, nonce), 0
+    pos = sorted(set(coin.draw() & (N - 1) for _ in range(queries)))
+    out = W()
+    for v in (Wd, 0, 0, logn, 0, 0, 16):
+        out.u8(v)
+    out.raw(P.to_bytes(16, "little"))  # field modulus bytes
+    for v in (queries, blowup, grind, ext, 2, 1, 0, 0, parts, rate, len(pos)):
+        out.u8(v)
+    cm = W()
+    for r_ in [ttree[1], ctree[1]] + roots + [rem_commit]:
+        cm.digest(r_)
+    out.vec(cm)
+
+    def put(w, v):
+        for x in F.flat(v):
+            w.fe(x)
+
+    tv, tp, cv, cp = W(), W(), W(), W()
+    for k in pos:
+        for c in range(Wd):
+            tv.fe(lde[c][k])
+        for j in range(Cc):
+            put(cv, clde[j][k])
+    _multiproof(tp, ttree, N, pos)
+    _multiproof(cp, ctree, N, pos)
+    out.usize(1)
+    for w in (tv, tp, cv, cp):
+        out.vec(w)
+    ts, es = W(), W()
+    for v in tz + tzg:
+        put(ts, v)
+    for v in hz + hzg:
+        put(es, v)
+    out.vec(ts)
+    out.vec(es)
+    out.usize(len(layers))
+    cur = pos
+    for d, lay in enumerate(layers):
+        h = len(lay) // 2
+        f = _fold_positions(cur, len(lay))
+        lv, lp = W(), W()
+        for y in f:
+            put(lv, lay[y])
+            put(lv, lay[y + h])
+        _multiproof(lp, trees[d], h, f)
+        out.vec(lv)
+        out.vec(lp)
+        cur = f
+    rv = W()
+    for v in rem:
+        put(rv, v)
+    out.vec(rv)
+    out.u8(0)
+    out.u64(nonce)
+    return bytes(out.b)
+
+
+def recursion_digest(ol, p):  # prove.rs:585-616
+    w = W()
+    w.raw(b"zkl/recursion/agg")
+    for k in ("suite", "batch_id", "children_root"):
+        w.raw(p[k])
+    w.u32(p["children_count"])
+    w.u64(p["v_units_total"])
+    _profile(w, p)
+    return ol.blake3(bytes(w.b))
+
+
+def _profile(w, p):
+    w.u32(p["m"]); w.u16(p["rho"]); w.u16(p["q"]); w.u16(p["o"]); w.u16(p["lam"]); w.u32(p["pi_len"])
+    w.u64(p["v_units"])
+    w.u32(p["lde_blowup"]); w.u8(p["folding"]); w.u8(p["redundancy"]); w.u8(p["num_layers"])
+    w.u16(p["num_queries"]); w.u32(p["grinding"])
+
+
+def encode_artifact(p, proof):  # lib.rs:486-551
+    w = W()
+    w.raw(b"ZKLRC1")
+    for k in ("program_id", "program_commitment", "pi_digest", "children_root", "batch_id"):
+        w.raw(p[k])
+    w.u64(p["v_units_total"])
+    w.u32(p["children_count"])
+    _profile(w, p)
+    w.raw(p["suite"])
+    w.u32(len(p["children_ms"]))
+    for m in p["children_ms"]:
+        w.u32(m)
+    for k in ("vm0", "vm1", "ru0", "ru1", "rs0", "rs1"):
+        w.raw(p[k])
+    for x in list(p["rom0"]) + list(p["rom1"]):
+        w.raw(x)
+    w.u32(len(proof))
+    w.raw(proof)
+    return bytes(w.b)
+
+
+def agg_prove(ol, step_bytes, queries=64, blowup=16, grind=16, min_security_bits=128):
+    """steps -> (ZKLRC1 artifact, recursion digest), as zkl_agg_prove."""
+    steps = [decode_step(ol, b) for b in step_bytes]
+    txs = [child_transcript(ol, s) for s in steps]
+    p = build_public(ol, steps)
+    T = agg_trace(ol, p, steps, txs)
+    q = max(queries, 16)
+    ext = 2 if min_security_bits >= 128 else 1
+    proof = prove_agg(ol, T, p, q, blowup, grind, ext)
+    return encode_artifact(p, proof), recursion_digest(ol, p), T

@@ -120,6 +120,8 @@ int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f
                             zkl_air_public_inputs *pi_out, uint32_t *width_out);
 
 /* ---------------- prover / verifier ---------------- */
+int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t log_n, uint32_t flags, const zkl_f128 *rom0_in,
+                               zkl_f128 *trace_out, zkl_air_public_inputs *pi_out, uint32_t *width_out);
 int orc_prove_segment(const zkl_f128 *trace, uint32_t width, uint32_t n,
                       const zkl_air_public_inputs *pi, const zkl_proof_options *opts,
                       uint8_t **proof, size_t *len, int boundary_mode);

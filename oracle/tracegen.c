@@ -237,6 +237,13 @@ static void ram_fill(zkl_f128 *t, size_t n, const zk_cols *c, const uint8_t pid[
 
 int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f128 *t, zkl_air_public_inputs *pi,
                             uint32_t *width_out) {
+  return orc_synth_vm_segment_chain(seed, seed, log_n, flags, NULL, t, pi, width_out);
+}
+
+/* the same with ROM lane 0 entering the first level at *rom0_in (the accumulator lane the
+ * aggregation chains across segments, agg/trace.rs:524-541) instead of 0 */
+int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t log_n, uint32_t flags, const zkl_f128 *rom0_in, zkl_f128 *t,
+                               zkl_air_public_inputs *pi, uint32_t *width_out) {
   if (log_n < 5 || log_n > 26 || (flags & ~7u)) return -1;
   if ((flags & SYN_MERKLE) && log_n < 8) return -1;
   size_t n = (size_t)1 << log_n, levels = n / 32;
@@ -250,7 +257,7 @@ int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f
   char desc[160];
   snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 %s%s%sseed=0x%016llx levels=%zu",
            (flags & SYN_SPONGE) ? "sponge " : "", (flags & SYN_RAM) ? "ram " : "", (flags & SYN_MERKLE) ? "merkle " : "",
-           (unsigned long long)seed, levels);
+           (unsigned long long)program_seed, levels);
   uint8_t pid[32];
   orc_blake3((const uint8_t *)desc, strlen(desc), pid);
   pos_suite ps;
@@ -406,7 +413,7 @@ int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f
     a = fe_exp(3, 1037); cur = fe_mul(a, 3);
     for (int i = 0; i < 59; i++) { w1[i] = cur; cur = fe_mul(cur, 3); }
   }
-  fe s0_prev = 0;
+  fe s0_prev = rom0_in ? ((fe)rom0_in->hi << 64 | rom0_in->lo) : 0;
   fe last_state[3] = {0, 0, 0};
   for (size_t l = 0; l < levels; l++) {
     size_t b = l * 32, rm = b, rf = b + 28;

@@ -186,6 +186,22 @@ def synth_segment(seed: int, log_n: int, flags: int = 0):
     return trace, pi, w.value
 
 
+def synth_segment_chain(program_seed: int, seed: int, log_n: int, rom0: int = 0, flags: int = 0):
+    """orc_synth_vm_segment_chain: segment `seed` of program `program_seed`, ROM lane 0
+    entering at rom0.  Returns (trace, AirPublicInputs, W)."""
+    w = C.c_uint32()
+    r0 = F128(rom0 & (2 ** 64 - 1), rom0 >> 64)
+    lib().orc_synth_vm_segment_chain(C.c_uint64(program_seed), C.c_uint64(seed), C.c_uint32(log_n),
+                                     C.c_uint32(flags), C.byref(r0), None, None, C.byref(w))
+    n = 1 << log_n
+    trace = (F128 * (w.value * n))()
+    pi = AirPublicInputs()
+    rc = lib().orc_synth_vm_segment_chain(C.c_uint64(program_seed), C.c_uint64(seed), C.c_uint32(log_n),
+                                          C.c_uint32(flags), C.byref(r0), trace, C.byref(pi), C.byref(w))
+    assert rc == 0
+    return trace, pi, w.value
+
+
 def default_options(width, n, queries=64, blowup=16, grind=16):
     parts = 16 if n >= 1 << 20 else 8 if n >= 1 << 18 else 4 if n >= 1 << 16 else 2 if n >= 1 << 14 else 1
     rate = 8 if width <= 32 else 16

@@ -2,6 +2,7 @@
 inputs; stage entry points agree with the oracle; full-size proofs are deterministic."""
 import ctypes as C
 import hashlib
+import os
 import random
 
 import pytest
@@ -661,3 +662,64 @@ def test_invalid_partition_options_rejected(gpu_ctx, field, value, msg):
     setattr(opts, field, value)
     with pytest.raises(zkl_hip.ZklError, match=msg):
         gpu_ctx.prove_segment(t, w, 64, pi, opts)
+
+
+def _chain():
+    import json
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "chain_2p16.json")
+    return json.load(open(p)) if os.path.exists(p) else None
+
+
+@pytest.mark.skipif(_chain() is None, reason="tests/golden/chain_2p16.json not generated")
+def test_chain_program_and_aggregation_match_goldens(oracle, gpu_ctx):
+    """BASELINE configs[2]/[3] shape end to end: the first 8 segments of the synthetic
+    multi-segment program (tests/golden/make_chain_goldens.py), proved on the GPU with 4
+    contexts in flight, equal the oracle goldens; their zl1 steps aggregate (zkl_agg_prove,
+    FieldExtension::Quadratic) into the golden ZKLRC1 artifact and recursion digest, and into
+    the artifact oracle/agg_ref.py builds from the GPU steps."""
+    import sys
+    import threading
+    import zkl_hip
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import agg_ref
+    ch = _chain()
+    n = 1 << ch["log_n"]
+    K = len(ch["segments"])
+    segs = [zkl_hip.synth_vm_segment_chain(ch["program_seed"], ch["program_seed"] + i, ch["log_n"],
+                                           int(ch["rom0_in"][i], 16)) for i in range(K)]
+    ctxs = [zkl_hip.Context(0) for _ in range(4)]
+    dev, got = [], [None] * K
+    for k, (t, pi, w) in enumerate(segs):
+        d = ctxs[k % 4].alloc(w * n * 16)
+        ctxs[k % 4].upload(d, t, w * n * 16)
+        dev.append(d)
+
+    def run(k):
+        for i in range(k, K, 4):
+            t, pi, w = segs[i]
+            got[i] = ctxs[k].prove_segment_device(dev[i], w, n, pi, zkl_hip.proof_options(w, n))
+
+    try:
+        th = [threading.Thread(target=run, args=(k,)) for k in range(4)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+    finally:
+        for k, d in enumerate(dev):
+            ctxs[k % 4].free(d)
+        for c in ctxs:
+            c.close()
+    for i, p in enumerate(got):
+        g = ch["segments"][i]
+        assert len(p) == g["len"] and hashlib.sha256(p).hexdigest() == g["sha256"], f"segment {i}"
+    steps = []
+    for i, ((t, pi, w), p) in enumerate(zip(segs, got)):
+        info = zkl_hip.step_info_for(pi, i, K, i.to_bytes(32, "little"), (i + 1).to_bytes(32, "little"))
+        steps.append(zkl_hip.step_proof_encode(pi, info, p))
+    art, dg = zkl_hip.agg_prove(steps)
+    ga = ch["aggregation"]
+    assert len(art) == ga["len"] and hashlib.sha256(art).hexdigest() == ga["sha256"]
+    assert dg.hex() == ga["recursion_digest"]
+    want, want_dg, _ = agg_ref.agg_prove(oracle, steps)
+    assert art == want and dg == want_dg

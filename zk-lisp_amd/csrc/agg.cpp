@@ -1,0 +1,1062 @@
+// Aggregation proof: what `zk-lisp prove` does after the segment
+// proofs exist -- RecursionPublicBuilder::build_public (lib.rs:404-482), RecursionBackend::
+// prove (lib.rs:295-344) and RecursionArtifactCodec::encode (lib.rs:486-551) of the
+// Winterfell backend:
+//   child transcripts      ZlChildTranscript::from_step + verify_child_transcript
+//                          (agg/child.rs:159-1023) over the Fiat-Shamir replay (agg/fs.rs:38-245)
+//   public inputs          AggAirPublicInputs (agg/pi.rs:20-218)
+//   aggregation trace      build_agg_trace_from_transcripts (agg/trace.rs:155-951,996-1685)
+//   AIR                    ZlAggAir: 24 transition constraints, 5 assertions, p_last (agg/air.rs)
+//   proof                  winterfell 0.13.1 Prover::prove with FieldExtension::Quadratic when
+//                          min_security_bits >= 128 (prove.rs:629-719), PoseidonHasher commitments
+//   artifact / digest      ZKLRC1 (lib.rs:486-551), recursion_digest_from_agg_pi (prove.rs:585-616)
+//
+// Where it runs: the aggregation trace has one row per child (>= 8 rows, 64 for BASELINE
+// configs[3]), so the whole proof is ~10^4 Poseidon permutations plus 2^16 grinding tries.
+// A GPU launch costs more than the work, so it stays on the host (the grinding search runs on
+// host threads); the segment proofs it consumes are the GPU's output.
+//
+// Quadratic extension (winter-math 0.13.1, f128 `ExtensibleField<2>` [WF-recall]): elements
+// a + b*phi with phi^2 = phi - 1, mul = [a0 b0 - a1 b1, (a0 + a1)(b0 + b1) - a0 b0], Frobenius
+// (a, b) -> (a + b, -b); serialised as two 16-byte base elements.  RandomCoin::draw::<E> reads
+// the 32 digest bytes as (a, b): the PoseidonHasher digest is a value plus 16 zero bytes, so every
+// drawn challenge has b = 0.  The arithmetic below is nevertheless the full extension field.
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/zkl_hip.h"
+#include "air_host.h"
+#include "host_hash.h"
+#include "host_proof.h"
+#include "proof_view.h"
+
+namespace zkl {
+
+void children_root(const uint8_t suite[32], const uint8_t* digests, const uint8_t* roots, size_t n, uint8_t out[32]);
+
+namespace {
+
+struct AggError : std::invalid_argument { using std::invalid_argument::invalid_argument; };
+
+// ------------------------------------------------------------------ quadratic extension
+struct fe2 {
+  fe a, b;
+};
+inline fe2 E(fe a) { return fe2{a, fe_zero()}; }
+inline fe2 add(fe2 x, fe2 y) { return {fe_add(x.a, y.a), fe_add(x.b, y.b)}; }
+inline fe2 sub(fe2 x, fe2 y) { return {fe_sub(x.a, y.a), fe_sub(x.b, y.b)}; }
+inline fe2 mul(fe2 x, fe2 y) {
+  const fe z = fe_mul(x.a, y.a);
+  return {fe_sub(z, fe_mul(x.b, y.b)), fe_sub(fe_mul(fe_add(x.a, x.b), fe_add(y.a, y.b)), z)};
+}
+inline fe2 mulb(fe2 x, fe s) { return {fe_mul(x.a, s), fe_mul(x.b, s)}; }
+inline fe2 inv(fe2 x) {  // conj / norm, norm = a^2 + a b + b^2
+  const fe nrm = fe_add(fe_add(fe_mul(x.a, x.a), fe_mul(x.a, x.b)), fe_mul(x.b, x.b));
+  if (fe_is_zero(nrm)) throw std::runtime_error("inversion of zero in the quadratic extension");
+  const fe ni = fe_inv(nrm);
+  return {fe_mul(fe_add(x.a, x.b), ni), fe_mul(fe_sub(fe_zero(), x.b), ni)};
+}
+inline bool is_zero(fe2 x) { return fe_is_zero(x.a) && fe_is_zero(x.b); }
+// base-field helpers with the same names, so the polynomial code below is generic
+inline fe add(fe x, fe y) { return fe_add(x, y); }
+inline fe sub(fe x, fe y) { return fe_sub(x, y); }
+inline fe mulb(fe x, fe s) { return fe_mul(x, s); }
+inline fe mul(fe x, fe y) { return fe_mul(x, y); }
+template <class T> T lift(fe x);
+template <> inline fe lift<fe>(fe x) { return x; }
+template <> inline fe2 lift<fe2>(fe x) { return E(x); }
+inline bool is_zero(fe x) { return fe_is_zero(x); }
+template <class T> T zero();
+template <> inline fe zero<fe>() { return fe_zero(); }
+template <> inline fe2 zero<fe2>() { return E(fe_zero()); }
+
+void put(Bytes& b, fe x) { b.felem(x); }
+void put(Bytes& b, fe2 x) { b.felem(x.a); b.felem(x.b); }
+void flat(std::vector<fe>& v, fe x) { v.push_back(x); }
+void flat(std::vector<fe>& v, fe2 x) { v.push_back(x.a); v.push_back(x.b); }
+
+// RandomCoin::draw::<QuadExtension<f128>>: the 32 digest bytes as (a, b) (b = the digest's
+// zero upper half)
+fe2 draw_e2(Coin& c) { return E(c.draw()); }
+
+// ------------------------------------------------------------------ polynomials (small, host)
+// in-place radix-2 NTT in natural order over <w_m>; inverse includes 1/m
+template <class T>
+void ntt(std::vector<T>& a, bool inverse) {
+  const size_t m = a.size();
+  const int lg = ilog2(m);
+  for (size_t i = 0, j = 0; i < m; i++) {
+    if (i < j) std::swap(a[i], a[j]);
+    size_t bit = m >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j |= bit;
+  }
+  for (int s = 1; s <= lg; s++) {
+    const size_t len = (size_t)1 << s, h = len / 2;
+    fe w = root_of_unity((unsigned)s);
+    if (inverse) w = fe_inv(w);
+    std::vector<fe> tw(h);
+    tw[0] = fe_one();
+    for (size_t k = 1; k < h; k++) tw[k] = fe_mul(tw[k - 1], w);
+    for (size_t i = 0; i < m; i += len)
+      for (size_t k = 0; k < h; k++) {
+        const T u = a[i + k], v = mulb(a[i + k + h], tw[k]);
+        a[i + k] = add(u, v);
+        a[i + k + h] = sub(u, v);
+      }
+  }
+  if (inverse) {
+    const fe mi = fe_inv(fe{m, 0});
+    for (auto& x : a) x = mulb(x, mi);
+  }
+}
+// values over offset * <w_m> -> coefficients
+template <class T>
+std::vector<T> interpolate(std::vector<T> v, fe offset) {
+  ntt(v, true);
+  const fe oi = fe_inv(offset);
+  fe p = fe_one();
+  for (auto& c : v) { c = mulb(c, p); p = fe_mul(p, oi); }
+  return v;
+}
+// coefficients (degree < m) -> values over offset * <w_M>, M >= m
+template <class T>
+std::vector<T> evaluate(const std::vector<T>& c, size_t M, fe offset) {
+  std::vector<T> v(M, zero<T>());
+  fe p = fe_one();
+  for (size_t k = 0; k < c.size(); k++) { v[k] = mulb(c[k], p); p = fe_mul(p, offset); }
+  ntt(v, false);
+  return v;
+}
+fe2 eval_at(const std::vector<fe>& c, fe2 x) {  // Horner, base coefficients at an extension point
+  fe2 acc = E(fe_zero());
+  for (size_t k = c.size(); k-- > 0;) acc = add(mul(acc, x), E(c[k]));
+  return acc;
+}
+fe2 eval_at(const std::vector<fe2>& c, fe2 x) {
+  fe2 acc = E(fe_zero());
+  for (size_t k = c.size(); k-- > 0;) acc = add(mul(acc, x), c[k]);
+  return acc;
+}
+
+// Merkle tree (winter-crypto MerkleTree): nodes[n + i] = leaf i, nodes[i] = merge(2i, 2i+1)
+std::vector<fe> merkle(const std::vector<fe>& leaves) {
+  const size_t n = leaves.size();
+  std::vector<fe> t(2 * n);
+  for (size_t i = 0; i < n; i++) t[n + i] = leaves[i];
+  for (size_t i = n; i-- > 1;) t[i] = hasher().merge(t[2 * i], t[2 * i + 1]);
+  return t;
+}
+void multiproof(Bytes& b, const std::vector<fe>& tree, size_t n_leaves, const std::vector<size_t>& idx) {
+  const Plan plan = batch_plan(n_leaves, idx);
+  b.u8((uint8_t)ilog2(n_leaves));
+  b.u8((uint8_t)plan.len.size());
+  size_t k = 0;
+  for (uint32_t l : plan.len) {
+    b.u8((uint8_t)l);
+    for (uint32_t j = 0; j < l; j++) b.digest(tree[plan.node[k++]]);
+  }
+}
+
+// ------------------------------------------------------------------ public inputs (agg/pi.rs)
+struct AggPi {
+  uint8_t program_id[32], program_commitment[32], pi_digest[32], children_root[32], batch_id[32];
+  uint64_t v_units_total = 0;
+  uint32_t children_count = 0;
+  // AggProfileMeta
+  uint32_t m = 0, pi_len = 0;
+  uint16_t rho = 0, q = 0, o = 0, lambda = 0;
+  uint64_t v_units = 0;
+  // AggFriProfile
+  uint32_t lde_blowup = 0;
+  uint8_t folding_factor = 2, redundancy = 1, num_layers = 1;
+  // AggQueryProfile
+  uint16_t num_queries = 0;
+  uint32_t grinding_factor = 0;
+  uint8_t suite_id[32];
+  std::vector<uint32_t> children_ms;
+  uint8_t vm_state_initial[32], vm_state_final[32];
+  uint8_t ram_u_initial[32], ram_u_final[32], ram_s_initial[32], ram_s_final[32];
+  uint8_t rom_initial[3][32], rom_final[3][32];
+};
+
+// AggAirPublicInputs::to_elements (agg/pi.rs:174-218)
+std::vector<fe> agg_pi_elements(const AggPi& p) {
+  std::vector<fe> o;
+  o.push_back(fold_bytes32(p.program_id));
+  o.push_back(fold_bytes32(p.program_commitment));
+  o.push_back(fold_bytes32(p.pi_digest));
+  o.push_back(fold_bytes32(p.children_root));
+  o.push_back(fold_bytes32(p.batch_id));
+  for (uint64_t v : {(uint64_t)p.m, (uint64_t)p.rho, (uint64_t)p.q, (uint64_t)p.o, (uint64_t)p.lambda, (uint64_t)p.pi_len,
+                     p.v_units, (uint64_t)p.lde_blowup, (uint64_t)p.folding_factor, (uint64_t)p.redundancy,
+                     (uint64_t)p.num_layers, (uint64_t)p.num_queries, (uint64_t)p.grinding_factor,
+                     (uint64_t)p.children_count, p.v_units_total})
+    o.push_back(fe{v, 0});
+  for (const uint8_t* b : {p.vm_state_initial, p.vm_state_final, p.ram_u_initial, p.ram_u_final, p.ram_s_initial,
+                           p.ram_s_final})
+    o.push_back(fold_bytes32(b));
+  for (int i = 0; i < 3; i++) o.push_back(fold_bytes32(p.rom_initial[i]));
+  for (int i = 0; i < 3; i++) o.push_back(fold_bytes32(p.rom_final[i]));
+  return o;
+}
+
+// zk_lisp_proof::pi::PublicInputs::digest (pi.rs:113-147) over the fields a step proof carries
+void pi_digest(const StepDecoded& s, uint8_t out[32]) {
+  Bytes b;
+  b.raw("zkl/pi/v1", 9);
+  b.raw(s.program_id, 32);
+  b.raw(s.program_commitment, 32);
+  b.raw(s.merkle_root, 32);
+  b.u64(s.feature_mask);
+  b.u32((uint32_t)s.main_args.size());
+  for (const zkl_vm_arg& a : s.main_args) {
+    b.u8((uint8_t)a.tag);
+    b.raw(a.bytes, a.tag == 0 ? 8 : a.tag == 1 ? 16 : 32);
+  }
+  blake3_hash(b.v.data(), b.v.size(), out);
+}
+
+// RecursionPublicBuilder::build_public (lib.rs:404-482); the caller's PublicInputs are the
+// ones every step carries (the builder requires all steps to share them)
+AggPi build_public(const std::vector<StepDecoded>& steps) {
+  if (steps.empty()) throw AggError("build_recursion_public requires at least one step");
+  const StepDecoded& f = steps.front();
+  for (const StepDecoded& s : steps) {
+    bool same = !memcmp(s.program_id, f.program_id, 32) && !memcmp(s.program_commitment, f.program_commitment, 32) &&
+                s.main_args.size() == f.main_args.size();
+    for (size_t i = 0; same && i < s.main_args.size(); i++)
+      same = s.main_args[i].tag == f.main_args[i].tag && !memcmp(s.main_args[i].bytes, f.main_args[i].bytes, 32);
+    if (!same)
+      throw AggError(
+          "build_recursion_public requires all steps to share the same program_id, program_commitment and main_args "
+          "as recursion public inputs");
+  }
+  AggPi p;
+  memcpy(p.program_id, f.program_id, 32);
+  memcpy(p.program_commitment, f.program_commitment, 32);
+  pi_digest(f, p.pi_digest);
+  std::vector<uint8_t> dg, rt;
+  for (const StepDecoded& s : steps) {
+    p.v_units_total = p.v_units_total + s.v_units < p.v_units_total ? ~0ull : p.v_units_total + s.v_units;
+    dg.insert(dg.end(), s.digest, s.digest + 32);
+    rt.insert(rt.end(), s.root_trace, s.root_trace + 32);
+    p.children_ms.push_back(s.m);
+  }
+  children_root(f.suite, dg.data(), rt.data(), steps.size(), p.children_root);
+  memset(p.batch_id, 0, 32);
+  p.children_count = (uint32_t)steps.size();
+  p.m = f.m; p.rho = f.rho; p.q = f.q; p.o = f.o; p.lambda = f.lambda; p.pi_len = f.pi_len; p.v_units = f.v_units;
+  p.lde_blowup = f.rho; p.folding_factor = 2; p.redundancy = 1; p.num_layers = 1;
+  p.num_queries = f.q; p.grinding_factor = 0;
+  memcpy(p.suite_id, f.suite, 32);
+  const StepDecoded& l = steps.back();
+  memcpy(p.vm_state_initial, f.bnd[0], 32);
+  memcpy(p.vm_state_final, l.bnd[1], 32);
+  memcpy(p.ram_u_initial, f.bnd[2], 32);
+  memcpy(p.ram_u_final, l.bnd[3], 32);
+  memcpy(p.ram_s_initial, f.bnd[4], 32);
+  memcpy(p.ram_s_final, l.bnd[5], 32);
+  for (int i = 0; i < 3; i++) {
+    memcpy(p.rom_initial[i], f.bnd[6 + i], 32);
+    memcpy(p.rom_final[i], l.bnd[9 + i], 32);
+  }
+  return p;
+}
+
+// recursion_digest_from_agg_pi (prove.rs:585-616)
+void recursion_digest(const AggPi& p, uint8_t out[32]) {
+  Bytes b;
+  b.raw("zkl/recursion/agg", 17);
+  b.raw(p.suite_id, 32);
+  b.raw(p.batch_id, 32);
+  b.raw(p.children_root, 32);
+  b.u32(p.children_count);
+  b.u64(p.v_units_total);
+  b.u32(p.m); b.u16(p.rho); b.u16(p.q); b.u16(p.o); b.u16(p.lambda); b.u32(p.pi_len); b.u64(p.v_units);
+  b.u32(p.lde_blowup); b.u8(p.folding_factor); b.u8(p.redundancy); b.u8(p.num_layers);
+  b.u16(p.num_queries); b.u32(p.grinding_factor);
+  blake3_hash(b.v.data(), b.v.size(), out);
+}
+
+// RecursionArtifactCodec::encode (lib.rs:486-551)
+std::vector<uint8_t> encode_artifact(const AggPi& p, const std::vector<uint8_t>& proof) {
+  Bytes b;
+  b.raw("ZKLRC1", 6);
+  b.raw(p.program_id, 32);
+  b.raw(p.program_commitment, 32);
+  b.raw(p.pi_digest, 32);
+  b.raw(p.children_root, 32);
+  b.raw(p.batch_id, 32);
+  b.u64(p.v_units_total);
+  b.u32(p.children_count);
+  b.u32(p.m); b.u16(p.rho); b.u16(p.q); b.u16(p.o); b.u16(p.lambda); b.u32(p.pi_len); b.u64(p.v_units);
+  b.u32(p.lde_blowup); b.u8(p.folding_factor); b.u8(p.redundancy); b.u8(p.num_layers);
+  b.u16(p.num_queries); b.u32(p.grinding_factor);
+  b.raw(p.suite_id, 32);
+  b.u32((uint32_t)p.children_ms.size());
+  for (uint32_t m : p.children_ms) b.u32(m);
+  for (const uint8_t* x : {p.vm_state_initial, p.vm_state_final, p.ram_u_initial, p.ram_u_final, p.ram_s_initial,
+                           p.ram_s_final})
+    b.raw(x, 32);
+  for (int i = 0; i < 3; i++) b.raw(p.rom_initial[i], 32);
+  for (int i = 0; i < 3; i++) b.raw(p.rom_final[i], 32);
+  b.u32((uint32_t)proof.size());
+  b.raw(proof.data(), proof.size());
+  return b.v;
+}
+
+// ------------------------------------------------------------------ child transcripts
+struct Child {
+  StepDecoded step;
+  SegmentView v;  // parsed and replayed inner proof (agg/child.rs:597-848 + agg/fs.rs:38-245)
+};
+
+// AirPublicInputs as replay_fs_from_step rebuilds them (agg/fs.rs:44-65): the step's core
+// public inputs, segment_feature_mask 0, boundary values from the zl1 public inputs
+zkl_air_public_inputs replay_pi(const StepDecoded& s) {
+  zkl_air_public_inputs pi{};
+  memcpy(pi.program_id, s.program_id, 32);
+  memcpy(pi.program_commitment, s.program_commitment, 32);
+  memcpy(pi.merkle_root, s.merkle_root, 32);
+  pi.feature_mask = s.feature_mask;
+  pi.segment_feature_mask = 0;
+  uint32_t k = 0;
+  auto slot = [&](fe v) {
+    if (k >= ZKL_MAX_MAIN_SLOTS) throw AggError("main_args exceed the supported slot count");
+    pi.main_slots[k++] = to_abi(v);
+  };
+  for (const zkl_vm_arg& a : s.main_args) {  // encode_vmarg_to_elements (utils.rs:79-97)
+    if (a.tag == 0) { uint64_t x; memcpy(&x, a.bytes, 8); slot(fe{x, 0}); }
+    else if (a.tag == 1) slot(be_from_le16(a.bytes));
+    else { slot(be_from_le16(a.bytes)); slot(be_from_le16(a.bytes + 16)); }
+  }
+  pi.n_main_slots = k;
+  for (int i = 0; i < 3; i++) pi.rom_acc[i] = to_abi(s.rom_acc[i]);
+  pi.pc_init = to_abi(be_from_le16(s.pc_init));
+  pi.ram_gp_unsorted_in = to_abi(be_from_le16(s.bnd[2]));
+  pi.ram_gp_unsorted_out = to_abi(be_from_le16(s.bnd[3]));
+  pi.ram_gp_sorted_in = to_abi(be_from_le16(s.bnd[4]));
+  pi.ram_gp_sorted_out = to_abi(be_from_le16(s.bnd[5]));
+  for (int i = 0; i < 3; i++) {
+    pi.rom_s_in[i] = to_abi(be_from_le16(s.bnd[6 + i]));
+    pi.rom_s_out[i] = to_abi(be_from_le16(s.bnd[9 + i]));
+  }
+  pi.vm_usage_mask = s.vm_usage_mask;
+  pi.ram_delta_clk_bits = s.ram_delta_clk_bits;
+  return pi;
+}
+
+Child load_child(const uint8_t* p, size_t n) {
+  Child c;
+  c.step = decode_step(p, n);
+  const zkl_air_public_inputs pi = replay_pi(c.step);
+  const std::string e = verify_segment_ex(c.step.inner, c.step.inner_len, pi, nullptr, &c.v, false);
+  if (!e.empty()) throw AggError("child step proof does not replay: " + e);
+  if (c.v.fri_roots.size() < 2) throw AggError("AggTrace requires at least two FRI layers per child");
+  return c;
+}
+
+// ------------------------------------------------------------------ aggregation trace
+// AggColumns::baseline (agg/layout.rs:97-175)
+enum AggCol {
+  C_OK, C_V0_SUM, C_V1_SUM, C_VNEXT_SUM, C_FRI_V0, C_FRI_V1, C_FRI_VNEXT, C_FRI_ALPHA, C_FRI_X0, C_FRI_X1, C_FRI_Q1,
+  C_COMP_SUM, C_ALPHA_DIV_ZM_SUM, C_MAP_L0_SUM, C_FINAL_LLAST_SUM, C_R, C_ALPHA, C_BETA, C_GAMMA, C_SEG_FIRST,
+  C_TRACE_ROOT_ERR, C_CONSTRAINT_ROOT_ERR, C_V_UNITS_ACC, C_V_UNITS_CHILD, C_CHILD_COUNT_ACC, C_VM_CHAIN_ERR,
+  C_RAM_U_CHAIN_ERR, C_RAM_S_CHAIN_ERR, C_ROM_CHAIN_ERR_0, C_ROM_CHAIN_ERR_1, C_ROM_CHAIN_ERR_2, AGG_W
+};
+constexpr size_t MIN_AGG_TRACE_ROWS = 8;
+
+// fold_positions_usize (agg/child.rs:1072-1100): pos mod (size / 2), deduplicated in order
+std::vector<size_t> fold_pos(const std::vector<size_t>& p, size_t size) {
+  std::vector<size_t> r;
+  for (size_t x : p) {
+    const size_t y = x % (size / 2);
+    if (std::find(r.begin(), r.end(), y) == r.end()) r.push_back(y);
+  }
+  return r;
+}
+size_t index_of(const std::vector<size_t>& v, size_t x) {
+  auto it = std::find(v.begin(), v.end(), x);
+  if (it == v.end()) throw AggError("FRI sample coset index not found in folded positions");
+  return (size_t)(it - v.begin());
+}
+// (x1 - x0) vnext == v1 (alpha - x0) - v0 (alpha - x1) at the coset of folded position y of a
+// layer of size `size` (constant domain offset, agg/trace.rs:759-821)
+fe fri_fold_at(fe v0, fe v1, fe alpha, size_t y, size_t size, fe* x0o = nullptr, fe* x1o = nullptr) {
+  const fe xe = fe_mul(fe_pow64(root_of_unity((unsigned)ilog2(size)), y), fe{3, 0});
+  const fe x0 = xe, x1 = fe_sub(fe_zero(), xe);
+  if (x0o) *x0o = x0;
+  if (x1o) *x1o = x1;
+  const fe num = fe_sub(fe_mul(v1, fe_sub(alpha, x0)), fe_mul(v0, fe_sub(alpha, x1)));
+  return fe_mul(num, fe_inv(fe_sub(x1, x0)));
+}
+// the value a layer of size `size` holds at position p (get_query_values geometry)
+fe layer_value(const SegmentView& v, int d, size_t p, size_t size) {
+  const size_t h = size / 2;
+  const size_t k = index_of(v.fri_positions[d], p % h);
+  return v.fri_values[d][2 * k + (p / h)];
+}
+
+// FS weights of the aggregation trace (agg/trace.rs:95-125)
+struct Weights { fe beta_deep, beta_fri_layer1, delta_depth, beta_paths; };
+Weights agg_weights(const AggPi& p) {
+  std::vector<fe> s = agg_pi_elements(p);
+  s.push_back(fe{0xA9, 0});
+  Coin c{hasher().hash_elements(s.data(), s.size()), 0};
+  Weights w;
+  w.beta_deep = c.draw();
+  w.beta_fri_layer1 = c.draw();
+  w.delta_depth = c.draw();
+  w.beta_paths = c.draw();
+  return w;
+}
+
+// compute_deep_agg_over_queries (agg/trace.rs:1126-1257)
+fe deep_value(const SegmentView& v, size_t k) {
+  const size_t W = v.width, Cc = (size_t)v.comp_cols, N = v.lde;
+  const fe x = fe_mul(fe_pow64(root_of_unity((unsigned)ilog2(N)), v.positions[k]), fe{3, 0});
+  const fe zg = fe_mul(v.z, root_of_unity((unsigned)ilog2(v.n)));
+  const fe iz = fe_inv(fe_sub(x, v.z)), izg = fe_inv(fe_sub(x, zg));
+  fe y = fe_zero();
+  for (size_t i = 0; i < W; i++) {
+    const fe t = v.trace_rows[k * W + i];
+    y = fe_add(y, fe_mul(v.deep_coeffs[i], fe_add(fe_mul(fe_sub(t, v.ood_trace_z[i]), iz),
+                                                  fe_mul(fe_sub(t, v.ood_trace_zg[i]), izg))));
+  }
+  for (size_t j = 0; j < Cc; j++) {
+    const fe c = v.comp_rows[k * Cc + j];
+    y = fe_add(y, fe_mul(v.deep_coeffs[W + j], fe_add(fe_mul(fe_sub(c, v.ood_comp_z[j]), iz),
+                                                      fe_mul(fe_sub(c, v.ood_comp_zg[j]), izg))));
+  }
+  return y;
+}
+fe deep_agg(const SegmentView& v, fe beta) {
+  fe acc = fe_zero(), bp = fe_one();
+  for (size_t k = 0; k < v.positions.size(); k++) {
+    const fe e = fe_sub(deep_value(v, k), layer_value(v, 0, v.positions[k], v.lde));
+    acc = fe_add(acc, fe_mul(bp, e));
+    bp = fe_mul(bp, beta);
+  }
+  return acc;
+}
+// compute_fri_layer1_agg_over_queries (agg/trace.rs:1261-1432)
+fe fri_layer1_agg(const SegmentView& v, fe beta) {
+  const size_t N = v.lde;
+  const auto& f0 = v.fri_positions[0];
+  fe acc = fe_zero(), bp = fe_one();
+  const size_t nk = std::min(f0.size(), v.positions.size());
+  for (size_t k = 0; k < nk; k++) {
+    const fe vn = fri_fold_at(v.fri_values[0][2 * k], v.fri_values[0][2 * k + 1], v.fri_alphas[0], f0[k], N);
+    acc = fe_add(acc, fe_mul(bp, fe_sub(vn, layer_value(v, 1, f0[k], N / 2))));
+    bp = fe_mul(bp, beta);
+  }
+  return acc;
+}
+// compute_fri_path_agg_over_layers (agg/trace.rs:697-951): one query path through every
+// layer and the remainder (Horner over the reversed coefficients at the constant offset)
+fe fri_path_agg(const SegmentView& v, fe delta, size_t s) {
+  const int nl = (int)v.fri_roots.size();
+  fe acc = fe_zero(), dp = fe_one(), v_rem = fe_zero();
+  size_t size = v.lde, pos_rem = 0;
+  for (int d = 0; d < nl; d++) {
+    const auto& f = v.fri_positions[d];
+    if (s >= f.size()) throw AggError("sample index out of bounds for FRI layer");
+    const fe vn = fri_fold_at(v.fri_values[d][2 * s], v.fri_values[d][2 * s + 1], v.fri_alphas[d], f[s], size);
+    if (d + 1 < nl) {
+      acc = fe_add(acc, fe_mul(dp, fe_sub(vn, layer_value(v, d + 1, f[s], size / 2))));
+      dp = fe_mul(dp, delta);
+    } else {
+      v_rem = vn;
+      pos_rem = f[s];
+    }
+    size /= 2;
+  }
+  const fe xl = fe_mul(fe{3, 0}, fe_pow64(root_of_unity((unsigned)ilog2(size)), pos_rem));
+  fe r = fe_zero();
+  for (const fe& c : v.remainder) r = fe_add(fe_mul(r, xl), c);
+  return fe_add(acc, fe_mul(dp, fe_sub(v_rem, r)));
+}
+fe fri_paths_agg(const SegmentView& v, fe delta, fe beta) {
+  size_t paths = ~(size_t)0;
+  for (const auto& f : v.fri_positions) paths = std::min(paths, f.size());
+  fe acc = fe_zero(), bp = fe_one();
+  for (size_t k = 0; k < paths; k++) {
+    acc = fe_add(acc, fe_mul(bp, fri_path_agg(v, delta, k)));
+    bp = fe_mul(bp, beta);
+  }
+  return acc;
+}
+
+// build_agg_trace_from_transcripts (agg/trace.rs:155-693): column-major AGG_W x rows
+std::vector<std::vector<fe>> build_agg_trace(const AggPi& p, const std::vector<Child>& ch) {
+  const size_t nc = ch.size();
+  if (nc == 0) throw AggError("AggTrace requires at least one child proof");
+  if (p.children_count != nc) throw AggError("AggAirPublicInputs.children_count must match number of children");
+  if (p.children_ms.size() != nc) throw AggError("AggAirPublicInputs.children_ms length must match number of children");
+  for (const Child& c : ch)
+    if (memcmp(c.step.suite, p.suite_id, 32))
+      throw AggError("AggAirPublicInputs.suite_id must match suite_id of all children");
+  const uint32_t total = ch[0].step.segments_total;
+  std::vector<uint32_t> idx;
+  for (const Child& c : ch) {
+    if (c.step.segments_total != total) throw AggError("AggTrace requires a uniform segments_total across children");
+    idx.push_back(c.step.segment_index);
+  }
+  if (total > 1) {
+    if (total != nc) throw AggError("AggTrace requires a complete contiguous segment chain in batch");
+    std::sort(idx.begin(), idx.end());
+    for (size_t i = 0; i < nc; i++)
+      if (idx[i] != i) throw AggError("AggTrace segment indices must form [0..children_count) without gaps");
+  }
+  for (const Child& c : ch) {
+    if (c.step.rho != p.rho || c.step.o != p.o || c.step.lambda != p.lambda || c.step.pi_len != p.pi_len)
+      throw AggError("AggAirPublicInputs.profile_meta is inconsistent with child StepMeta");
+    if (c.step.q != p.num_queries)
+      throw AggError("AggAirPublicInputs.profile_queries.num_queries is inconsistent with child meta.q");
+  }
+  {
+    std::vector<uint8_t> dg, rt;
+    for (const Child& c : ch) {
+      dg.insert(dg.end(), c.step.digest, c.step.digest + 32);
+      rt.insert(rt.end(), c.step.root_trace, c.step.root_trace + 32);
+    }
+    uint8_t root[32];
+    children_root(p.suite_id, dg.data(), rt.data(), nc, root);
+    if (memcmp(root, p.children_root, 32))
+      throw AggError("AggAirPublicInputs.children_root is inconsistent with child commitments");
+  }
+  uint64_t vsum = 0;
+  for (size_t i = 0; i < nc; i++) {
+    if (p.children_ms[i] == 0) throw AggError("AggAirPublicInputs.children_ms entries must be non-zero");
+    if (p.children_ms[i] != ch[i].step.m) throw AggError("AggAirPublicInputs.children_ms entry does not match child meta.m");
+    if (vsum + ch[i].step.v_units < vsum) throw AggError("AggAirPublicInputs.v_units_total overflow");
+    vsum += ch[i].step.v_units;
+  }
+  if (vsum != p.v_units_total) throw AggError("AggAirPublicInputs.v_units_total must equal sum of child meta.v_units");
+
+  size_t rows = 1;
+  while (rows < std::max(nc, MIN_AGG_TRACE_ROWS)) rows *= 2;
+  std::vector<std::vector<fe>> T(AGG_W, std::vector<fe>(rows, fe_zero()));
+  const fe vm0 = fold_bytes32(p.vm_state_initial), vm1 = fold_bytes32(p.vm_state_final);
+  const fe ru0 = fold_bytes32(p.ram_u_initial), ru1 = fold_bytes32(p.ram_u_final);
+  const fe rs0 = fold_bytes32(p.ram_s_initial), rs1 = fold_bytes32(p.ram_s_final);
+  const fe ro0 = fold_bytes32(p.rom_initial[0]), ro1 = fold_bytes32(p.rom_final[0]);
+  fe v_acc = fe_zero(), cnt = fe_zero(), pvm{}, pru{}, prs{}, pro{};
+  const Weights w = agg_weights(p);
+  for (size_t i = 0; i < nc; i++) {
+    const StepDecoded& s = ch[i].step;
+    const fe vm_in = fold_bytes32(s.bnd[0]), vm_out = fold_bytes32(s.bnd[1]);
+    const fe ru_in = fold_bytes32(s.bnd[2]), ru_out = fold_bytes32(s.bnd[3]);
+    const fe rs_in = fold_bytes32(s.bnd[4]), rs_out = fold_bytes32(s.bnd[5]);
+    const fe ro_in = fold_bytes32(s.bnd[6]), ro_out = fold_bytes32(s.bnd[9]);  // lane 0 only (trace.rs:524-541)
+    fe vm_err = fe_sub(vm_in, i ? pvm : vm0), ru_err = fe_sub(ru_in, i ? pru : ru0), rs_err = fe_sub(rs_in, i ? prs : rs0);
+    fe ro_err = fe_sub(ro_in, i ? pro : ro0);
+    if (i + 1 == nc) {
+      ro_err = fe_add(ro_err, fe_sub(ro_out, ro1));
+      vm_err = fe_add(vm_err, fe_sub(vm_out, vm1));
+      ru_err = fe_add(ru_err, fe_sub(ru_out, ru1));
+      rs_err = fe_add(rs_err, fe_sub(rs_out, rs1));
+    }
+    T[C_SEG_FIRST][i] = fe_one();
+    T[C_V_UNITS_CHILD][i] = fe{s.v_units, 0};
+    T[C_V_UNITS_ACC][i] = v_acc;
+    T[C_CHILD_COUNT_ACC][i] = cnt;
+    // trace_root_err / constraint_root_err: sum over queries of the root each opening
+    // reproduces minus the committed root; the replay verified every opening against its root
+    // under the library's row-digest rule, so both sums are zero here
+    T[C_TRACE_ROOT_ERR][i] = fe_zero();
+    T[C_CONSTRAINT_ROOT_ERR][i] = fe_zero();
+    T[C_VM_CHAIN_ERR][i] = vm_err;
+    T[C_RAM_U_CHAIN_ERR][i] = ru_err;
+    T[C_RAM_S_CHAIN_ERR][i] = rs_err;
+    T[C_ROM_CHAIN_ERR_0][i] = ro_err;
+    // per-child FRI / DEEP overlay (trace.rs:187-235, sample_fri_fold_child :1436-1685)
+    const SegmentView& v = ch[i].v;
+    const size_t N = v.lde, y0 = v.fri_positions[0][0];
+    fe x0, x1;
+    const fe v0 = v.fri_values[0][0], v1 = v.fri_values[0][1], alpha = v.fri_alphas[0];
+    const fe vn = fri_fold_at(v0, v1, alpha, y0, N, &x0, &x1);
+    T[C_FRI_V0][i] = v0;
+    T[C_FRI_V1][i] = v1;
+    T[C_FRI_VNEXT][i] = vn;
+    T[C_FRI_ALPHA][i] = alpha;
+    T[C_FRI_X0][i] = x0;
+    T[C_FRI_X1][i] = x1;
+    T[C_FRI_Q1][i] = layer_value(v, 1, y0, N / 2);
+    T[C_COMP_SUM][i] = deep_agg(v, w.beta_deep);
+    T[C_ALPHA_DIV_ZM_SUM][i] = fri_layer1_agg(v, w.beta_fri_layer1);
+    T[C_MAP_L0_SUM][i] = fri_path_agg(v, w.delta_depth, 0);
+    T[C_FINAL_LLAST_SUM][i] = fri_paths_agg(v, w.delta_depth, w.beta_paths);
+    v_acc = fe_add(v_acc, fe{s.v_units, 0});
+    cnt = fe_add(cnt, fe_one());
+    pvm = vm_out; pru = ru_out; prs = rs_out; pro = ro_out;
+  }
+  for (size_t r = nc; r < rows; r++) {
+    T[C_V_UNITS_ACC][r] = v_acc;
+    T[C_CHILD_COUNT_ACC][r] = cnt;
+  }
+  return T;
+}
+
+// ------------------------------------------------------------------ ZlAggAir (agg/air.rs)
+constexpr int AGG_TC = 24;
+struct Deg { int base; bool cycle; };  // cycle: one periodic column of period trace_len
+const Deg kAggDegrees[AGG_TC] = {{1, false}, {2, true}, {1, false}, {1, false}, {1, false}, {1, false},
+                                 {1, false}, {1, false}, {1, false}, {1, false}, {1, false}, {1, true},
+                                 {1, false}, {1, false}, {1, false}, {1, false}, {1, false}, {1, false},
+                                 {1, false}, {1, false}, {1, false}, {1, false}, {1, false}, {1, false}};
+
+// evaluate_transition (agg/air.rs:113-274) on base-field frames
+void agg_transition(const fe* c, const fe* nx, fe is_last, fe r[AGG_TC]) {
+  const fe nl = fe_sub(fe_one(), is_last);
+  auto chain = [&](int col) { return fe_mul(nl, fe_sub(nx[col], c[col])); };
+  r[0] = c[C_OK];
+  r[1] = fe_mul(nl, fe_sub(nx[C_V_UNITS_ACC], fe_add(c[C_V_UNITS_ACC], fe_mul(c[C_V_UNITS_CHILD], c[C_SEG_FIRST]))));
+  r[2] = c[C_TRACE_ROOT_ERR];
+  r[3] = c[C_CONSTRAINT_ROOT_ERR];
+  r[4] = chain(C_R);
+  r[5] = chain(C_ALPHA);
+  r[6] = chain(C_BETA);
+  r[7] = chain(C_GAMMA);
+  r[8] = chain(C_V0_SUM);
+  r[9] = chain(C_V1_SUM);
+  r[10] = chain(C_VNEXT_SUM);
+  r[11] = fe_mul(nl, fe_sub(nx[C_CHILD_COUNT_ACC], fe_add(c[C_CHILD_COUNT_ACC], c[C_SEG_FIRST])));
+  const fe xd = fe_sub(c[C_FRI_X1], c[C_FRI_X0]);
+  r[12] = fe_sub(fe_mul(c[C_FRI_VNEXT], xd), fe_sub(fe_mul(c[C_FRI_V1], fe_sub(c[C_FRI_ALPHA], c[C_FRI_X0])),
+                                                   fe_mul(c[C_FRI_V0], fe_sub(c[C_FRI_ALPHA], c[C_FRI_X1]))));
+  r[13] = fe_sub(c[C_FRI_VNEXT], c[C_FRI_Q1]);
+  r[14] = c[C_COMP_SUM];
+  r[15] = c[C_ALPHA_DIV_ZM_SUM];
+  r[16] = c[C_MAP_L0_SUM];
+  r[17] = c[C_FINAL_LLAST_SUM];
+  r[18] = c[C_VM_CHAIN_ERR];
+  r[19] = c[C_RAM_U_CHAIN_ERR];
+  r[20] = c[C_RAM_S_CHAIN_ERR];
+  r[21] = c[C_ROM_CHAIN_ERR_0];
+  r[22] = c[C_ROM_CHAIN_ERR_1];
+  r[23] = c[C_ROM_CHAIN_ERR_2];
+}
+
+struct AggOpts { uint32_t queries, blowup, grind, field_ext; };
+
+// winterfell 0.13.1 Prover::prove for ZlAggAir over E = QuadExtension<f128> (or E = f128 when
+// the security target is below 128 bits: FieldExtension::None, prove.rs:647-651)
+template <class T>
+std::vector<uint8_t> prove_air(const std::vector<std::vector<fe>>& trace, const std::vector<fe>& pi_el, const AggPi& pi,
+                               const AggOpts& ao) {
+  const Hasher& H = hasher();
+  const size_t W = trace.size(), n = trace[0].size();
+  const int logn = ilog2(n);
+  const size_t B = ao.blowup, N = n * B;
+  if (B < 2 || (B & (B - 1)) || B > 128) throw AggError("aggregation blowup must be a power of two in [2, 128]");
+  zkl_proof_options o{};
+  o.num_queries = ao.queries;
+  o.blowup_factor = ao.blowup;
+  o.grinding_factor = ao.grind;
+  o.field_extension = ao.field_ext;
+  o.fri_folding_factor = 2;
+  o.fri_remainder_max_degree = 1;
+  o.batching_constraints = 0;
+  o.batching_deep = 0;
+  zkl_select_partitions((uint32_t)W, (uint32_t)n, &o.num_partitions, &o.hash_rate);
+  auto draw = [](Coin& c) -> T {
+    if constexpr (sizeof(T) == sizeof(fe2)) return draw_e2(c);
+    else return c.draw();
+  };
+  auto put_flat = [](std::vector<fe>& v, const T& x) { flat(v, x); };
+
+  // AirContext: evaluation degrees, CE blowup, composition columns (winter-air [WF-recall])
+  size_t max_eval = 0, ceb = 2;
+  for (const Deg& d : kAggDegrees) {
+    max_eval = std::max(max_eval, (size_t)d.base * (n - 1) + (d.cycle ? n - 1 : 0));
+    size_t mb = 1;
+    while (mb < (size_t)(d.base + (d.cycle ? 1 : 0) - 1)) mb *= 2;
+    ceb = std::max(ceb, mb);
+  }
+  if (B < ceb) throw AggError("aggregation blowup below the constraint-evaluation blowup");
+  const size_t Cc = std::max<size_t>(1, (max_eval - (n - 1) + n - 1) / n);
+  const size_t ce = n * ceb;
+  const fe off{3, 0}, g = root_of_unity((unsigned)logn), gl = fe_pow64(g, n - 1);
+
+  std::vector<fe> seed = context_elements((uint32_t)W, n, o);
+  seed.insert(seed.end(), pi_el.begin(), pi_el.end());
+  Coin coin{H.hash_elements(seed.data(), seed.size()), 0};
+
+  // 0. the trace must satisfy the AIR (winterfell validates this in debug builds; the
+  // composition degree bound C n equals the CE domain here, so a violated constraint would
+  // otherwise only surface as a proof the verifier rejects)
+  {
+    std::vector<fe> cur(W), nxt(W);
+    fe tc[AGG_TC];
+    for (size_t i = 0; i + 1 < n; i++) {  // one transition exemption: the last row is not checked
+      for (size_t c = 0; c < W; c++) { cur[c] = trace[c][i]; nxt[c] = trace[c][i + 1]; }
+      agg_transition(cur.data(), nxt.data(), i == n - 1 ? fe_one() : fe_zero(), tc);
+      for (int k = 0; k < AGG_TC; k++)
+        if (!fe_is_zero(tc[k]))
+          throw AggError("aggregation trace does not satisfy ZlAggAir: transition constraint C" + std::to_string(k) +
+                         " fails at row " + std::to_string(i));
+    }
+    const size_t last = n - 1;
+    const bool ok = fe_is_zero(trace[C_OK][0]) && fe_is_zero(trace[C_V_UNITS_ACC][0]) &&
+                    fe_is_zero(trace[C_CHILD_COUNT_ACC][0]) && fe_eq(trace[C_V_UNITS_ACC][last], fe{pi.v_units_total, 0}) &&
+                    fe_eq(trace[C_CHILD_COUNT_ACC][last], fe{pi.children_count, 0});
+    if (!ok) throw AggError("aggregation trace does not satisfy ZlAggAir: an assertion fails");
+  }
+
+  // 1. trace LDE + commitment (rows hashed whole: one partition)
+  std::vector<std::vector<fe>> tpoly(W), lde(W);
+  for (size_t c = 0; c < W; c++) {
+    tpoly[c] = interpolate(trace[c], fe_one());
+    lde[c] = evaluate(tpoly[c], N, off);
+  }
+  // select_partitions_for_trace gives one partition below 2^14 rows (a batch of <= 2^13
+  // children), so partition_size == width and a row digest is hash_elements(row)
+  if (o.num_partitions != 1) throw AggError("aggregation traces of 2^14 rows or more are not supported");
+  std::vector<fe> leaves(N);
+  {
+    std::vector<fe> row(W);
+    for (size_t i = 0; i < N; i++) {
+      for (size_t c = 0; c < W; c++) row[c] = lde[c][i];
+      leaves[i] = H.hash_elements(row.data(), W);
+    }
+  }
+  const std::vector<fe> ttree = merkle(leaves);
+  coin.reseed(ttree[1]);
+
+  // 2. constraint composition coefficients, evaluation over the CE coset
+  const int na = 5;
+  std::vector<T> alpha(AGG_TC), beta(na);
+  for (auto& a : alpha) a = draw(coin);
+  for (auto& b : beta) b = draw(coin);
+  // get_assertions (agg/air.rs:276-304) sorted by (step, column)
+  struct As { size_t col, step; fe v; };
+  const size_t last = n - 1;
+  std::vector<As> asr = {{C_OK, 0, fe_zero()},
+                         {C_V_UNITS_ACC, 0, fe_zero()},
+                         {C_CHILD_COUNT_ACC, 0, fe_zero()},
+                         {C_V_UNITS_ACC, last, fe{pi.v_units_total, 0}},
+                         {C_CHILD_COUNT_ACC, last, fe{pi.children_count, 0}}};
+  std::vector<T> cev(ce);
+  {
+    const fe wce = root_of_unity((unsigned)ilog2(ce));
+    fe x = off;
+    const size_t step = N / ce;
+    std::vector<fe> cur(W), nxt(W);
+    fe tc[AGG_TC];
+    for (size_t i = 0; i < ce; i++, x = fe_mul(x, wce)) {
+      for (size_t c = 0; c < W; c++) {
+        cur[c] = lde[c][i * step];
+        nxt[c] = lde[c][(i * step + B) % N];
+      }
+      const fe xn = fe_pow64(x, n), xg = fe_sub(x, gl);
+      const fe p_last = fe_mul(fe_mul(gl, fe_sub(xn, fe_one())), fe_inv(fe_mul(fe{n, 0}, xg)));
+      agg_transition(cur.data(), nxt.data(), p_last, tc);
+      T t = zero<T>();
+      for (int k = 0; k < AGG_TC; k++) t = add(t, mulb(alpha[k], tc[k]));
+      t = mulb(t, fe_mul(xg, fe_inv(fe_sub(xn, fe_one()))));
+      for (size_t a = 0; a < asr.size(); a++)
+        t = add(t, mulb(beta[a], fe_mul(fe_sub(cur[asr[a].col], asr[a].v), fe_inv(fe_sub(x, fe_pow64(g, asr[a].step))))));
+      cev[i] = t;
+    }
+  }
+  // 3. composition polynomial: coset interpolation, degree check, column split, LDE, commitment
+  std::vector<T> cco = interpolate(cev, off);
+  for (size_t k = Cc * n; k < ce; k++)
+    if (!is_zero(cco[k])) throw AggError("aggregation trace does not satisfy ZlAggAir (composition degree too large)");
+  std::vector<std::vector<T>> hpoly(Cc), clde(Cc);
+  for (size_t j = 0; j < Cc; j++) {
+    hpoly[j].assign(cco.begin() + (long)(j * n), cco.begin() + (long)((j + 1) * n));
+    clde[j] = evaluate(hpoly[j], N, off);
+  }
+  std::vector<fe> cleaves(N);
+  {
+    std::vector<fe> row;
+    for (size_t i = 0; i < N; i++) {
+      row.clear();
+      for (size_t j = 0; j < Cc; j++) put_flat(row, clde[j][i]);
+      cleaves[i] = H.hash_elements(row.data(), row.size());  // one partition: the whole row
+    }
+  }
+  const std::vector<fe> ctree = merkle(cleaves);
+  coin.reseed(ctree[1]);
+
+  // 4. out-of-domain frame
+  const T z = draw(coin);
+  fe2 z2, zg2;
+  if constexpr (sizeof(T) == sizeof(fe2)) z2 = z; else z2 = E(z);
+  zg2 = mul(z2, E(g));
+  std::vector<fe2> tz(W), tzg(W), hz(Cc), hzg(Cc);
+  for (size_t c = 0; c < W; c++) { tz[c] = eval_at(tpoly[c], z2); tzg[c] = eval_at(tpoly[c], zg2); }
+  for (size_t j = 0; j < Cc; j++) {
+    std::vector<fe2> hp(n);
+    for (size_t k = 0; k < n; k++) {
+      if constexpr (sizeof(T) == sizeof(fe2)) hp[k] = hpoly[j][k]; else hp[k] = E(hpoly[j][k]);
+    }
+    hz[j] = eval_at(hp, z2);
+    hzg[j] = eval_at(hp, zg2);
+  }
+  auto as_T = [](fe2 v) -> T {
+    if constexpr (sizeof(T) == sizeof(fe2)) return v;
+    else return v.a;  // base-field proof: the point is a base element, so are the evaluations
+  };
+  {
+    std::vector<fe> oc;  // trace(z) | H(z) | trace(zg) | H(zg)  (agg/fs.rs:152-164)
+    for (auto& v : tz) put_flat(oc, as_T(v));
+    for (auto& v : hz) put_flat(oc, as_T(v));
+    for (auto& v : tzg) put_flat(oc, as_T(v));
+    for (auto& v : hzg) put_flat(oc, as_T(v));
+    coin.reseed(H.hash_elements(oc.data(), oc.size()));
+  }
+  // 5. DEEP composition over the LDE domain
+  std::vector<T> gam(W + Cc);
+  for (auto& c : gam) c = draw(coin);
+  std::vector<T> ev(N);
+  {
+    const fe wN = root_of_unity((unsigned)ilog2(N));
+    fe x = off;
+    for (size_t i = 0; i < N; i++, x = fe_mul(x, wN)) {
+      const fe2 iz = inv(sub(E(x), z2)), izg = inv(sub(E(x), zg2));
+      fe2 y = E(fe_zero());
+      for (size_t c = 0; c < W; c++) {
+        const fe2 t = E(lde[c][i]);
+        const fe2 term = add(mul(sub(t, tz[c]), iz), mul(sub(t, tzg[c]), izg));
+        fe2 gc;
+        if constexpr (sizeof(T) == sizeof(fe2)) gc = gam[c]; else gc = E(gam[c]);
+        y = add(y, mul(gc, term));
+      }
+      for (size_t j = 0; j < Cc; j++) {
+        fe2 hv, gc;
+        if constexpr (sizeof(T) == sizeof(fe2)) { hv = clde[j][i]; gc = gam[W + j]; }
+        else { hv = E(clde[j][i]); gc = E(gam[W + j]); }
+        const fe2 term = add(mul(sub(hv, hz[j]), iz), mul(sub(hv, hzg[j]), izg));
+        y = add(y, mul(gc, term));
+      }
+      ev[i] = as_T(y);
+    }
+  }
+  // 6. FRI (folding 2, constant domain offset, remainder degree 1)
+  const size_t rem_max = (size_t)(o.fri_remainder_max_degree + 1) * B;
+  std::vector<std::vector<T>> layers;
+  std::vector<std::vector<fe>> ftrees;
+  std::vector<fe> fri_roots;
+  while (ev.size() > rem_max) {
+    const size_t Nd = ev.size(), h = Nd / 2;
+    std::vector<fe> lf(h), row;
+    for (size_t i = 0; i < h; i++) {
+      row.clear();
+      put_flat(row, ev[i]);
+      put_flat(row, ev[i + h]);
+      lf[i] = H.hash_elements(row.data(), row.size());
+    }
+    ftrees.push_back(merkle(lf));
+    fri_roots.push_back(ftrees.back()[1]);
+    coin.reseed(fri_roots.back());
+    const T a = draw(coin);
+    const fe wd = root_of_unity((unsigned)ilog2(Nd));
+    std::vector<T> nx(h);
+    fe xe = off;
+    for (size_t i = 0; i < h; i++, xe = fe_mul(xe, wd)) {
+      const fe x0 = xe, x1 = fe_sub(fe_zero(), xe);
+      // (v1 (a - x0) - v0 (a - x1)) / (x1 - x0)
+      const T num = sub(mul(ev[i + h], sub(a, lift<T>(x0))), mul(ev[i], sub(a, lift<T>(x1))));
+      nx[i] = mulb(num, fe_inv(fe_sub(x1, x0)));
+    }
+    layers.push_back(std::move(ev));
+    ev = std::move(nx);
+  }
+  const int nl = (int)layers.size();
+  std::vector<T> rco = interpolate(ev, off);
+  const size_t rlen = o.fri_remainder_max_degree + 1;
+  for (size_t k = rlen; k < rco.size(); k++)
+    if (!is_zero(rco[k])) throw AggError("FRI remainder degree exceeds the remainder bound");
+  std::vector<T> rem(rlen);
+  for (size_t k = 0; k < rlen; k++) rem[k] = rco[rlen - 1 - k];
+  fe rem_commit;
+  {
+    std::vector<fe> rf;
+    for (auto& v : rem) put_flat(rf, v);
+    rem_commit = H.hash_elements(rf.data(), rf.size());
+  }
+  coin.reseed(rem_commit);
+
+  // 7. grinding: smallest nonce >= 1 (host threads; winterfell without `concurrent` searches
+  // sequentially, so the minimum is what it finds)
+  uint64_t nonce = 1;
+  if (ao.grind > 0) {
+    const fe sd = coin.seed;
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const uint64_t chunk = 4096;
+    std::atomic<uint64_t> next{1}, best{~0ull};
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; t++)
+      th.emplace_back([&] {
+        for (;;) {
+          const uint64_t b0 = next.fetch_add(chunk);
+          if (b0 > best.load()) return;
+          for (uint64_t x = b0; x < b0 + chunk; x++) {
+            const fe d = H.merge_with_int(sd, x);
+            const uint32_t tz = d.lo ? (uint32_t)__builtin_ctzll(d.lo) : 64u;
+            if (tz >= ao.grind) {
+              uint64_t cur = best.load();
+              while (x < cur && !best.compare_exchange_weak(cur, x)) {}
+              break;
+            }
+          }
+        }
+      });
+    for (auto& t : th) t.join();
+    nonce = best.load();
+  }
+  // 8. query positions: draw_integers(q, N, nonce), sort, dedup
+  coin.seed = H.merge_with_int(coin.seed, nonce);
+  coin.counter = 0;
+  std::vector<size_t> pos;
+  for (uint32_t k = 0; k < ao.queries; k++) pos.push_back((size_t)(coin.draw().lo & (N - 1)));
+  std::sort(pos.begin(), pos.end());
+  pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
+  const size_t nq = pos.size();
+
+  // 9. Proof::to_bytes (the segment prover's layout; extension elements as two base elements)
+  Bytes P;
+  P.u8((uint8_t)W); P.u8(0); P.u8(0); P.u8((uint8_t)logn); P.u8(0); P.u8(0);
+  P.u8(16); P.felem(fe{P_LO, P_HI});
+  P.u8((uint8_t)o.num_queries); P.u8((uint8_t)o.blowup_factor); P.u8((uint8_t)o.grinding_factor);
+  P.u8((uint8_t)o.field_extension); P.u8((uint8_t)o.fri_folding_factor); P.u8((uint8_t)o.fri_remainder_max_degree);
+  P.u8((uint8_t)o.batching_constraints); P.u8((uint8_t)o.batching_deep);
+  P.u8((uint8_t)o.num_partitions); P.u8((uint8_t)o.hash_rate);
+  P.u8((uint8_t)nq);
+  {
+    Bytes cm;
+    cm.digest(ttree[1]); cm.digest(ctree[1]);
+    for (auto& r : fri_roots) cm.digest(r);
+    cm.digest(rem_commit);
+    P.vec(cm);
+  }
+  Bytes tv, tp, cv, cpb;
+  for (size_t k : pos) for (size_t c = 0; c < W; c++) tv.felem(lde[c][k]);
+  for (size_t k : pos) for (size_t j = 0; j < Cc; j++) put(cv, clde[j][k]);
+  multiproof(tp, ttree, N, pos);
+  multiproof(cpb, ctree, N, pos);
+  P.usize(1);
+  P.vec(tv); P.vec(tp);
+  P.vec(cv); P.vec(cpb);
+  {
+    Bytes ts, es;
+    for (auto& v : tz) put(ts, as_T(v));
+    for (auto& v : tzg) put(ts, as_T(v));
+    for (auto& v : hz) put(es, as_T(v));
+    for (auto& v : hzg) put(es, as_T(v));
+    P.vec(ts); P.vec(es);
+  }
+  P.usize((uint64_t)nl);
+  {
+    std::vector<size_t> p = pos;
+    for (int d = 0; d < nl; d++) {
+      const size_t Nd = layers[d].size(), h = Nd / 2;
+      std::vector<size_t> f;
+      for (size_t x : p) { const size_t y = x % h; if (std::find(f.begin(), f.end(), y) == f.end()) f.push_back(y); }
+      Bytes lv, lp;
+      for (size_t y : f) { put(lv, layers[d][y]); put(lv, layers[d][y + h]); }
+      multiproof(lp, ftrees[d], h, f);
+      P.vec(lv); P.vec(lp);
+      p = f;
+    }
+  }
+  {
+    Bytes rv;
+    for (auto& v : rem) put(rv, v);
+    P.vec(rv);
+  }
+  P.u8(0);  // FriProof num_partitions (log2 of 1)
+  P.u64(nonce);
+  return P.v;
+}
+
+}  // namespace
+}  // namespace zkl
+
+// ====================================================================== C ABI
+using namespace zkl;
+
+namespace {
+std::vector<Child> load_children(const uint8_t* const* steps, const size_t* lens, uint32_t n) {
+  if (!steps || !lens || n == 0) throw AggError("RecursionBackend::recursion_prove requires at least one step proof");
+  std::vector<Child> ch;
+  ch.reserve(n);
+  for (uint32_t i = 0; i < n; i++) {
+    if (!steps[i]) throw AggError("null step proof");
+    ch.push_back(load_child(steps[i], lens[i]));
+  }
+  for (const Child& c : ch)
+    if (memcmp(c.step.suite, ch[0].step.suite, 32))
+      throw AggError("RecursionBackend::recursion_prove requires all steps to share the same suite_id");
+  return ch;
+}
+AggPi public_of(const std::vector<Child>& ch) {
+  std::vector<StepDecoded> st;
+  for (const Child& c : ch) st.push_back(c.step);
+  return build_public(st);
+}
+}  // namespace
+
+extern "C" {
+
+int zkl_agg_prove(const uint8_t* const* steps, const size_t* step_lens, uint32_t n_steps, const zkl_agg_options* opts,
+                  uint8_t** artifact_out, size_t* artifact_len, uint8_t digest_out[32]) {
+  if (!opts || !artifact_out || !artifact_len) return ZKL_E_INVALID;
+  std::vector<uint8_t> art;
+  const int rc = guarded_call([&] {
+    const std::vector<Child> ch = load_children(steps, step_lens, n_steps);
+    const AggPi pi = public_of(ch);  // build_public; prove() re-derives suite / count / ms identically
+    const auto T = build_agg_trace(pi, ch);
+    AggOpts ao{std::max<uint32_t>(opts->queries, 16), opts->blowup, opts->grind,
+               opts->min_security_bits >= 128 ? 2u : 1u};
+    if (ao.queries > 255) throw AggError("queries must be at most 255");
+    if (opts->min_security_bits >= 64) {  // estimate_conjectured_security_bits (prove.rs:1177-1195)
+      const uint32_t field = 128 * (ao.field_ext == 2 ? 2 : 1);
+      uint32_t qs = (uint32_t)ilog2(ao.blowup) * ao.queries;
+      if (qs >= 80) qs += ao.grind;
+      const uint32_t bits = std::min(std::min(field, qs) - 1, 128u);
+      if (bits < opts->min_security_bits)
+        throw AggError(
+            "aggregation prover options do not achieve requested min_security_bits; increase --queries/--blowup/--grind "
+            "or lower --security-bits");
+    }
+    const std::vector<fe> el = agg_pi_elements(pi);
+    const std::vector<uint8_t> proof =
+        ao.field_ext == 2 ? prove_air<fe2>(T, el, pi, ao) : prove_air<fe>(T, el, pi, ao);
+    art = encode_artifact(pi, proof);
+    if (digest_out) recursion_digest(pi, digest_out);
+  });
+  if (rc) return rc;
+  *artifact_out = (uint8_t*)malloc(art.size());
+  if (!*artifact_out) return ZKL_E_OOM;
+  memcpy(*artifact_out, art.data(), art.size());
+  *artifact_len = art.size();
+  return ZKL_OK;
+}
+
+int zkl_agg_trace(const uint8_t* const* steps, const size_t* step_lens, uint32_t n_steps, zkl_f128* out,
+                  uint32_t max_rows, uint32_t* rows_out) {
+  if (!rows_out) return ZKL_E_INVALID;
+  return guarded_call([&] {
+    const std::vector<Child> ch = load_children(steps, step_lens, n_steps);
+    const auto T = build_agg_trace(public_of(ch), ch);
+    const uint32_t rows = (uint32_t)T[0].size();
+    *rows_out = rows;
+    if (!out) return;
+    if (rows > max_rows) throw AggError("output buffer too small for the aggregation trace");
+    for (size_t c = 0; c < T.size(); c++)
+      for (uint32_t r = 0; r < rows; r++) out[c * rows + r] = to_abi(T[c][r]);
+  });
+}
+
+}  // extern "C"

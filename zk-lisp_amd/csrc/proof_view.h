@@ -7,6 +7,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -64,5 +65,38 @@ struct SegmentView {
 // first failing check otherwise; `view` (optional) receives the parsed/replayed values.
 std::string verify_segment(const uint8_t* proof, size_t len, const zkl_air_public_inputs& pi,
                            const zkl_proof_options& opts, SegmentView* view);
+// The same with the options taken from the proof (opts == nullptr) and, when check_ood is
+// false, without the out-of-domain constraint identity: the Fiat-Shamir replay plus every
+// opening / DEEP / FRI / remainder / PoW check, which is what the aggregation re-derives from
+// a step proof alone (agg/fs.rs:38-245 rebuilds the AIR public inputs without the expected
+// VM output, so the identity is not available there either).
+std::string verify_segment_ex(const uint8_t* proof, size_t len, const zkl_air_public_inputs& pi,
+                              const zkl_proof_options* opts, SegmentView* view, bool check_ood);
+
+// A decoded ZKLSTP1 step proof (StepProof::from_bytes, proof/step.rs:153-493) with the
+// derived StepMeta (step.rs:516-533), zl1 root_trace (format.rs:214-238) and step digest
+// (proof/digest.rs:16-68).  `inner` points into the caller's buffer.
+struct StepDecoded {
+  uint32_t lambda_bits = 0;
+  uint8_t suite[32], program_id[32], program_commitment[32], merkle_root[32];
+  uint64_t feature_mask = 0;
+  std::vector<zkl_vm_arg> main_args;
+  uint32_t vm_usage_mask = 0, ram_delta_clk_bits = 0;
+  fe rom_acc[3];
+  uint32_t segment_index = 0, segments_total = 1;  // new_single_segment normalises to (0, 1)
+  uint8_t pc_init[32];
+  // state_in, state_out, ram_gp_unsorted_in/out, ram_gp_sorted_in/out, rom_s_in[3], rom_s_out[3]
+  uint8_t bnd[12][32];
+  const uint8_t* inner = nullptr;
+  size_t inner_len = 0;
+  uint32_t m = 0, pi_len = 0;
+  uint16_t rho = 0, q = 0, o = 0, lambda = 0;
+  uint64_t v_units = 0;
+  uint8_t digest[32], root_trace[32];
+};
+StepDecoded decode_step(const uint8_t* p, size_t n);
+
+// runs f, mapping exceptions to ZKL_E_* codes and zkl_hip_last_error(NULL) (prover.cpp)
+int guarded_call(const std::function<void()>& f);
 
 }  // namespace zkl

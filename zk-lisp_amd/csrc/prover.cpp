@@ -21,6 +21,7 @@
 #include "air_host.h"
 #include "host_hash.h"
 #include "kernels.h"
+#include "host_proof.h"
 #include "proof_view.h"
 
 using namespace zkl;
@@ -38,7 +39,6 @@ namespace {
 
 struct InvalidArg : std::runtime_error { using std::runtime_error::runtime_error; };
 
-int ilog2(size_t n) { int k = 0; while (((size_t)1 << k) < n) k++; return k; }
 uint32_t bitrev_u(uint32_t x, int logn) { uint32_t r = 0; for (int i = 0; i < logn; i++) r |= ((x >> i) & 1u) << (logn - 1 - i); return r; }
 
 // ------------------------------------------------------------------ device buffers
@@ -75,87 +75,6 @@ struct HBuf {
   T* at(size_t off = 0) const { return (T*)((char*)p + off); }
   ~HBuf() { if (p) (void)hipHostFree(p); }
 };
-
-// ------------------------------------------------------------------ Fiat-Shamir coin
-// DefaultRandomCoin<PoseidonHasher> [WF-recall]; order pinned by agg/fs.rs:67-237.
-struct Coin {
-  fe seed;
-  uint64_t counter = 0;
-  void reseed(fe d) { seed = hasher().merge(seed, d); counter = 0; }
-  fe draw() { return hasher().merge_with_int(seed, ++counter); }
-};
-
-// ------------------------------------------------------------------ byte writer
-struct Bytes {
-  std::vector<uint8_t> v;
-  void u8(uint8_t x) { v.push_back(x); }
-  void raw(const void* p, size_t n) {
-    const size_t o = v.size();
-    v.resize(o + n);
-    memcpy(v.data() + o, p, n);
-  }
-  void u64(uint64_t x) {  // little-endian host (x86-64 / gfx950 hosts)
-    raw(&x, 8);
-  }
-  void usize(uint64_t x) {  // winter-utils write_usize (vint64)
-    int lz = x ? __builtin_clzll(x) : 64;
-    int l = (lz > 0 ? lz - 1 : 0) / 7;
-    int len = 9 - std::min(l, 8);
-    if (len == 9) { u8(0); u64(x); return; }
-    uint64_t enc = ((x << 1) | 1) << (len - 1);
-    raw(&enc, (size_t)len);
-  }
-  void felem(fe x) {
-    const uint64_t w[2] = {x.lo, x.hi};
-    raw(w, 16);
-  }
-  void digest(fe x) {
-    const uint64_t w[4] = {x.lo, x.hi, 0, 0};
-    raw(w, 32);
-  }
-  void vec(const Bytes& b) { usize(b.v.size()); raw(b.v.data(), b.v.size()); }
-};
-
-// MerkleTree::prove_batch node-index plan (winter-crypto 0.13, [WF-recall]):
-// returns, per normalized leaf pair, the list of tree-node indices whose digests go in.
-// Leaves are tree nodes n+i.
-struct Plan {
-  std::vector<uint64_t> node;  // the lists back to back
-  std::vector<uint32_t> len;   // entries per list
-};
-Plan batch_plan(size_t n_leaves, const std::vector<size_t>& idx) {
-  const int depth = ilog2(n_leaves);
-  std::vector<size_t> norm(idx.size()), req(idx);
-  for (size_t k = 0; k < idx.size(); k++) norm[k] = idx[k] & ~(size_t)1;
-  std::sort(norm.begin(), norm.end());
-  norm.erase(std::unique(norm.begin(), norm.end()), norm.end());
-  std::sort(req.begin(), req.end());
-  // list k takes at most two leaves and one node per level: fixed-stride scratch, compacted
-  const size_t L = norm.size(), stride = (size_t)depth + 2;
-  std::vector<uint64_t> tmp(L * stride);
-  std::vector<uint32_t> cnt(L, 0);
-  std::vector<size_t> cur(L), next;
-  next.reserve(L);
-  for (size_t k = 0; k < L; k++) {
-    for (size_t j = norm[k]; j < norm[k] + 2; j++)
-      if (!std::binary_search(req.begin(), req.end(), j)) tmp[k * stride + cnt[k]++] = n_leaves + j;
-    cur[k] = (norm[k] + n_leaves) >> 1;
-  }
-  for (int lvl = 1; lvl < depth; lvl++) {
-    next.clear();
-    for (size_t i = 0; i < cur.size(); i++) {
-      size_t sib = cur[i] ^ 1;
-      if (i + 1 < cur.size() && cur[i + 1] == sib) i++;
-      else tmp[i * stride + cnt[i]++] = sib;
-      next.push_back(sib >> 1);
-    }
-    cur.swap(next);
-  }
-  Plan P;
-  P.len = cnt;
-  for (size_t k = 0; k < L; k++) P.node.insert(P.node.end(), tmp.begin() + k * stride, tmp.begin() + k * stride + cnt[k]);
-  return P;
-}
 
 }  // namespace
 
@@ -895,6 +814,10 @@ int run_guarded(zkl_ctx* ctx, const std::function<void()>& f) {
 }
 
 }  // namespace
+
+// context-free ABI entry points of other translation units (agg.cpp) report through the same
+// thread-local last-error string
+int zkl::guarded_call(const std::function<void()>& f) { return run_guarded(nullptr, f); }
 
 // ====================================================================== C ABI
 extern "C" {

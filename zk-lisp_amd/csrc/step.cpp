@@ -3,6 +3,8 @@
 // (step.rs:153-493), the zl1 commitment echo root_trace (proof/format.rs:214-238) and the
 // step digest (proof/digest.rs:16-68).  Host-only byte work; the inner proof is the
 // Proof::to_bytes image written by prover.cpp.
+#include <string.h>
+
 #include <algorithm>
 #include <stdexcept>
 #include <string>
@@ -11,6 +13,7 @@
 #include "../../include/zkl_hip.h"
 #include "field.h"
 #include "host_hash.h"
+#include "proof_view.h"
 
 namespace zkl {
 
@@ -166,70 +169,83 @@ std::vector<uint8_t> step_encode(const zkl_air_public_inputs& pi, const zkl_step
   return o.v;
 }
 
-void step_digest(const uint8_t* p, size_t n, uint8_t digest[32], uint8_t rt[32]) {
+StepDecoded decode_step(const uint8_t* p, size_t n) {
   In r{p, n};
   if (n < 7) throw std::invalid_argument("step proof too short to contain magic header");
   if (std::string((const char*)p, 7) != "ZKLSTP1") throw std::invalid_argument("invalid step proof magic tag");
   r.off = 7;
-  const uint32_t lambda_bits = r.u32("lambda_bits");
-  const uint8_t* suite = r.take(32, "suite_id bytes");
-  const uint8_t* program_id = r.take(32, "program_id bytes");
-  const uint8_t* program_commitment = r.take(32, "program_commitment bytes");
-  r.take(32, "merkle_root bytes");
-  const uint64_t feature_mask = r.u64("feature_mask");
+  StepDecoded D;
+  D.lambda_bits = r.u32("lambda_bits");
+  memcpy(D.suite, r.take(32, "suite_id bytes"), 32);
+  memcpy(D.program_id, r.take(32, "program_id bytes"), 32);
+  memcpy(D.program_commitment, r.take(32, "program_commitment bytes"), 32);
+  memcpy(D.merkle_root, r.take(32, "merkle_root bytes"), 32);
+  D.feature_mask = r.u64("feature_mask");
   const uint32_t nargs = r.u32("main_args length");
   size_t slots = 0;
   for (uint32_t i = 0; i < nargs; i++) {
     const uint8_t tag = *r.take(1, "VmArg tag");
     if (tag > 2) throw std::invalid_argument("invalid VmArg tag in step proof encoding");
-    r.take(tag == 0 ? 8 : tag == 1 ? 16 : 32, tag == 0 ? "VmArg::U64" : tag == 1 ? "VmArg::U128" : "VmArg::Bytes32");
+    const size_t len = tag == 0 ? 8 : tag == 1 ? 16 : 32;
+    zkl_vm_arg a{};
+    a.tag = tag;
+    memcpy(a.bytes, r.take(len, tag == 0 ? "VmArg::U64" : tag == 1 ? "VmArg::U128" : "VmArg::Bytes32"), len);
+    D.main_args.push_back(a);
     slots += arg_slots(tag);
   }
-  r.u32("vm_usage_mask");
-  r.u32("ram_delta_clk_bits");
-  r.take(96, "rom_acc bytes");
-  uint32_t seg_index = r.u32("segment_index");
-  uint32_t seg_total = r.u32("segments_total");
-  const uint8_t* pc_init = r.take(32, "pc_init bytes");
-  const uint8_t* bnd = r.take(32 * 12, "state_in_hash bytes");  // state in/out, ram gp x4, rom in/out x3
+  D.vm_usage_mask = r.u32("vm_usage_mask");
+  D.ram_delta_clk_bits = r.u32("ram_delta_clk_bits");
+  const uint8_t* ra = r.take(96, "rom_acc bytes");
+  for (int i = 0; i < 3; i++) D.rom_acc[i] = be_from_le16(ra + 32 * i);  // fe_from_bytes_fold (utils.rs:386-390)
+  D.segment_index = r.u32("segment_index");
+  D.segments_total = r.u32("segments_total");
+  memcpy(D.pc_init, r.take(32, "pc_init bytes"), 32);
+  memcpy(D.bnd, r.take(32 * 12, "state_in_hash bytes"), 32 * 12);  // state in/out, ram gp x4, rom in/out x3
   const uint32_t inner_len = r.u32("inner proof length");
-  const uint8_t* inner = r.take(inner_len, "inner proof bytes");
-  const InnerView v = view_inner(inner, inner_len);
-  if (seg_total <= 1) { seg_index = 0; seg_total = 1; }  // new_single_segment (step.rs:413-432)
-
-  uint8_t rtb[32];
-  root_trace(suite, v, rtb);
-  if (rt) for (int i = 0; i < 32; i++) rt[i] = rtb[i];
-  if (!digest) return;
+  D.inner = r.take(inner_len, "inner proof bytes");
+  D.inner_len = inner_len;
+  const InnerView v = view_inner(D.inner, D.inner_len);
+  if (D.segments_total <= 1) { D.segment_index = 0; D.segments_total = 1; }  // new_single_segment (step.rs:413-432)
+  root_trace(D.suite, v, D.root_trace);
 
   // StepMeta::from_env (step.rs:516-533): m, rho, q, o = 2, lambda, pi_len (5 + slots + 13
   // elements of AirPublicInputs::to_elements, lib.rs:116-160), v_units = m q
-  const uint32_t m = 1u << v.log_n;
-  const uint16_t rho = (uint16_t)v.blowup, q = (uint16_t)v.queries, oo = 2;
-  const uint16_t lambda = (uint16_t)(lambda_bits > 65535 ? 65535 : lambda_bits);
-  const uint32_t pi_len = (uint32_t)(5 + slots + 13);
+  D.m = 1u << v.log_n;
+  D.rho = (uint16_t)v.blowup;
+  D.q = (uint16_t)v.queries;
+  D.o = 2;
+  D.lambda = (uint16_t)(D.lambda_bits > 65535 ? 65535 : D.lambda_bits);
+  D.pi_len = (uint32_t)(5 + slots + 13);
+  D.v_units = (uint64_t)D.m * D.q;
   Out mb;
-  mb.u32(m); mb.u16(rho); mb.u16(q); mb.u16(oo); mb.u16(lambda); mb.u32(pi_len); mb.u64((uint64_t)m * q);
+  mb.u32(D.m); mb.u16(D.rho); mb.u16(D.q); mb.u16(D.o); mb.u16(D.lambda); mb.u32(D.pi_len); mb.u64(D.v_units);
   Out pb;
-  pb.b32(program_id);
-  pb.b32(program_commitment);
-  pb.u64(feature_mask);
-  pb.u32(seg_index);
-  pb.u32(seg_total);
-  pb.b32(pc_init);
-  pb.raw(bnd, 32 * 12);
+  pb.b32(D.program_id);
+  pb.b32(D.program_commitment);
+  pb.u64(D.feature_mask);
+  pb.u32(D.segment_index);
+  pb.u32(D.segments_total);
+  pb.b32(D.pc_init);
+  pb.raw(D.bnd, 32 * 12);
 
-  const PoseidonSuite S = derive_poseidon_suite(suite, 27);
-  const fe suite_fe = ro_from_parts("zkl/step/digest/suite", {std::vector<uint8_t>(suite, suite + 32)});
+  const PoseidonSuite S = derive_poseidon_suite(D.suite, 27);
+  const fe suite_fe = ro_from_parts("zkl/step/digest/suite", {std::vector<uint8_t>(D.suite, D.suite + 32)});
   const fe h_meta = two_lanes(S, ro_from_parts("zkl/step/digest/meta", {mb.v}), fe_zero());
   const fe h_pi = two_lanes(S, ro_from_parts("zkl/step/digest/pi", {pb.v}), fe_zero());
-  const fe h_roots = two_lanes(S, fold_bytes32(rtb), fe_zero());
+  const fe h_roots = two_lanes(S, fold_bytes32(D.root_trace), fe_zero());
   const fe c0 = two_lanes(S, suite_fe, h_meta);
   const fe c1 = two_lanes(S, c0, h_pi);
   const fe ch = two_lanes(S, c1, h_roots);
   Out d;
   d.fe_fold(ch);
-  for (int i = 0; i < 32; i++) digest[i] = d.v[i];
+  memcpy(D.digest, d.v.data(), 32);
+  return D;
+}
+
+void step_digest(const uint8_t* p, size_t n, uint8_t digest[32], uint8_t rt[32]) {
+  const StepDecoded D = decode_step(p, n);
+  if (rt) memcpy(rt, D.root_trace, 32);
+  if (digest) memcpy(digest, D.digest, 32);
 }
 
 // agg::child::children_root_from_compact (agg/child.rs:853-895): leaf_i =

@@ -221,6 +221,11 @@ extern "C" int zkl_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128* tra
 
 extern "C" int zkl_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f128* trace,
                                        zkl_air_public_inputs* pi, uint32_t* width_out) {
+  return zkl_synth_vm_segment_chain(seed, seed, log_n, flags, nullptr, trace, pi, width_out);
+}
+
+extern "C" int zkl_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t log_n, uint32_t flags, const zkl_f128* rom0_in,
+                                          zkl_f128* trace, zkl_air_public_inputs* pi, uint32_t* width_out) {
   const uint32_t all = ZKL_SYN_SPONGE | ZKL_SYN_RAM | ZKL_SYN_MERKLE;
   if ((flags & ~all) || log_n < 5 || log_n > 26) return ZKL_E_INVALID;
   if ((flags & ZKL_SYN_MERKLE) && log_n < 8) return ZKL_E_INVALID;  // the path needs 8 levels
@@ -236,7 +241,7 @@ extern "C" int zkl_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t f
 
   char desc[160];
   snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 %s%s%sseed=0x%016llx levels=%zu",
-           sponge ? "sponge " : "", ram ? "ram " : "", merkle ? "merkle " : "", (unsigned long long)seed, levels);
+           sponge ? "sponge " : "", ram ? "ram " : "", merkle ? "merkle " : "", (unsigned long long)program_seed, levels);
   uint8_t pid[32];
   blake3_hash((const uint8_t*)desc, strlen(desc), pid);
   PoseidonSuite ps = derive_poseidon_suite(pid, 27);
@@ -385,7 +390,7 @@ extern "C" int zkl_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t f
     for (int q = 0; q < 5; q++) for (int i = 0; i < 8; i++) s = fe_add(s, fe_mul(T.get(st[q] + i, row), w[k++]));
     return s;
   };
-  fe s0_prev = fe_zero();
+  fe s0_prev = rom0_in ? fe_from(*rom0_in) : fe_zero();  // ROM lane 0 carries across segments
   fe last[3] = {};
   for (size_t l = 0; l < levels; l++) {
     size_t b = l * 32, rm = b, rf = b + 28;

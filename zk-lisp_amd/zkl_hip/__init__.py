@@ -17,6 +17,8 @@ __all__ = [
     "select_partitions_for_trace", "proof_options", "synth_vm_segment", "STAGE_NAMES",
     "FM_VM", "FM_VM_EXPECT", "FM_POSEIDON", "FM_SPONGE", "FM_MERKLE", "FM_RAM",
     "VmArg", "StepInfo", "check_request", "row_digest_rule", "verify_segment", "step_proof_encode", "step_proof_digest", "parse_step_proof", "children_root",
+    "AggOptions", "agg_prove", "agg_trace", "parse_agg_artifact", "synth_segment_chain", "synth_vm_segment_chain",
+    "step_info_for",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -151,8 +153,151 @@ def load_library():
     lib.zkl_step_proof_digest.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_void_p]
     lib.zkl_children_root.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_uint32, C.c_void_p]
     lib.zkl_hip_lde.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]
+    lib.zkl_synth_vm_segment_chain.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, P(F128), C.c_void_p,
+                                               P(AirPublicInputs), P(C.c_uint32)]
+    lib.zkl_agg_prove.argtypes = [P(C.c_char_p), P(C.c_size_t), C.c_uint32, P(AggOptions), P(P(C.c_uint8)),
+                                  P(C.c_size_t), C.c_void_p]
+    lib.zkl_agg_trace.argtypes = [P(C.c_char_p), P(C.c_size_t), C.c_uint32, C.c_void_p, C.c_uint32, P(C.c_uint32)]
     _lib = lib
     return lib
+
+
+class AggOptions(C.Structure):
+    """zk_lisp_proof::ProverOptions as the aggregation reads it (zk-lisp-proof/src/lib.rs:40-66)."""
+    _fields_ = [("queries", C.c_uint32), ("blowup", C.c_uint32), ("grind", C.c_uint32),
+                ("min_security_bits", C.c_uint32)]
+
+
+def _steps_args(steps):
+    arr = (C.c_char_p * len(steps))(*[bytes(s) for s in steps])
+    lens = (C.c_size_t * len(steps))(*[len(s) for s in steps])
+    return arr, lens
+
+
+def agg_prove(steps, queries=64, blowup=16, grind=16, min_security_bits=128):
+    """RecursionPublicBuilder::build_public + RecursionBackend::prove + RecursionArtifactCodec::
+    encode (lib.rs:295-551): ZKLSTP1 step proofs -> (ZKLRC1 artifact, recursion digest)."""
+    lib = load_library()
+    arr, lens = _steps_args(steps)
+    o = AggOptions(queries, blowup, grind, min_security_bits)
+    out, ln, dg = C.POINTER(C.c_uint8)(), C.c_size_t(), (C.c_uint8 * 32)()
+    rc = lib.zkl_agg_prove(arr, lens, len(steps), C.byref(o), C.byref(out), C.byref(ln), dg)
+    if rc:
+        raise ZklError(rc, lib.zkl_hip_last_error(None).decode(errors="replace"))
+    data = C.string_at(out, ln.value)
+    lib.zkl_hip_free(out)
+    return data, bytes(dg)
+
+
+def agg_trace(steps):
+    """build_agg_trace_from_transcripts (agg/trace.rs:155-238): 31 column lists of ints."""
+    lib = load_library()
+    arr, lens = _steps_args(steps)
+    rows = C.c_uint32()
+    rc = lib.zkl_agg_trace(arr, lens, len(steps), None, 0, C.byref(rows))
+    if rc:
+        raise ZklError(rc, lib.zkl_hip_last_error(None).decode(errors="replace"))
+    buf = (F128 * (31 * rows.value))()
+    rc = lib.zkl_agg_trace(arr, lens, len(steps), C.cast(buf, C.c_void_p), rows.value, C.byref(rows))
+    if rc:
+        raise ZklError(rc, lib.zkl_hip_last_error(None).decode(errors="replace"))
+    r = rows.value
+    return [[buf[c * r + i].lo | (buf[c * r + i].hi << 64) for i in range(r)] for c in range(31)]
+
+
+def parse_agg_artifact(b: bytes) -> dict:
+    """RecursionArtifactCodec::decode (lib.rs:552-...) field order: the ZKLRC1 public inputs and
+    the aggregation proof bytes."""
+    import struct
+    if b[:6] != b"ZKLRC1":
+        raise ValueError("invalid recursion artifact magic")
+    off = 6
+
+    def take(k):
+        nonlocal off
+        if off + k > len(b):
+            raise ValueError("recursion artifact truncated")
+        off += k
+        return b[off - k:off]
+
+    d = {k: take(32) for k in ("program_id", "program_commitment", "pi_digest", "children_root", "batch_id")}
+    d["v_units_total"], d["children_count"] = struct.unpack("<QI", take(12))
+    d["m"], d["rho"], d["q"], d["o"], d["lambda"], d["pi_len"], d["v_units"] = struct.unpack("<IHHHHIQ", take(24))
+    d["lde_blowup"], d["folding_factor"], d["redundancy"], d["num_layers"] = struct.unpack("<IBBB", take(7))
+    d["num_queries"], d["grinding_factor"] = struct.unpack("<HI", take(6))
+    d["suite_id"] = take(32)
+    n_ms = struct.unpack("<I", take(4))[0]
+    d["children_ms"] = list(struct.unpack(f"<{n_ms}I", take(4 * n_ms)))
+    for k in ("vm_state_initial", "vm_state_final", "ram_gp_unsorted_initial", "ram_gp_unsorted_final",
+              "ram_gp_sorted_initial", "ram_gp_sorted_final"):
+        d[k] = take(32)
+    d["rom_s_initial"] = [take(32) for _ in range(3)]
+    d["rom_s_final"] = [take(32) for _ in range(3)]
+    d["proof"] = take(struct.unpack("<I", take(4))[0])
+    if off != len(b):
+        raise ValueError("trailing bytes after the recursion artifact")
+    return d
+
+
+def step_info_for(pi: AirPublicInputs, index: int, total: int, state_in: bytes, state_out: bytes,
+                  lambda_bits: int = 128) -> "StepInfo":
+    """zl1 step metadata as prove_segment fills it (prove.rs:1103-1174): suite = program_id
+    (prove.rs:985), the segment boundary bytes fe_to_bytes_fold of the AIR public inputs'
+    pc_init / RAM grand products / ROM lanes (SegmentBoundaryBytes, prove.rs:1112), and the VM
+    state hashes of the trace builder (here given)."""
+    info = StepInfo()
+    info.suite_id[:] = bytes(pi.program_id)
+    info.lambda_bits, info.segment_index, info.segments_total = lambda_bits, index, total
+
+    def fold(v):
+        return (v.lo | (v.hi << 64)).to_bytes(16, "little") + bytes(16)
+
+    info.pc_init[:] = fold(pi.pc_init)
+    info.state_in_hash[:] = bytes(state_in)
+    info.state_out_hash[:] = bytes(state_out)
+    for f in ("ram_gp_unsorted_in", "ram_gp_unsorted_out", "ram_gp_sorted_in", "ram_gp_sorted_out"):
+        getattr(info, f)[:] = fold(getattr(pi, f))
+    for i in range(3):
+        info.rom_s_in[i][:] = fold(pi.rom_s_in[i])
+        info.rom_s_out[i][:] = fold(pi.rom_s_out[i])
+    return info
+
+
+def synth_vm_segment_chain(program_seed: int, seed: int, log_n: int, rom0: int = 0, flags: int = 0):
+    """One segment of a synthetic multi-segment program (zkl_synth_vm_segment_chain): program
+    identity from program_seed, ops from seed, ROM lane 0 entering at rom0.  (trace, pi, width)."""
+    lib = load_library()
+    w = C.c_uint32()
+    r0 = F128(rom0 & (2 ** 64 - 1), rom0 >> 64)
+    lib.zkl_synth_vm_segment_chain(program_seed, seed, log_n, flags, C.byref(r0), None, None, C.byref(w))
+    trace = (F128 * (w.value * (1 << log_n)))()
+    pi = AirPublicInputs()
+    rc = lib.zkl_synth_vm_segment_chain(program_seed, seed, log_n, flags, C.byref(r0), C.cast(trace, C.c_void_p),
+                                        C.byref(pi), C.byref(w))
+    if rc != 0:
+        raise ZklError(rc, "synth_vm_segment_chain failed")
+    return trace, pi, w.value
+
+
+def synth_segment_chain(seed: int, log_n: int, count: int, flags: int = 0):
+    """`count` synthetic segments of one program (program id from `seed`, ops from seed + i) whose
+    ROM accumulator lane 0 carries from one to the next (zkl_synth_vm_segment_chain):
+    [(trace, pi, width)]; segment i+1 starts where segment i's
+    rom_s_out[0] ended, as the aggregation's ROM chain requires (agg/trace.rs:524-541)."""
+    lib = load_library()
+    out, rom0 = [], F128(0, 0)
+    for i in range(count):
+        w = C.c_uint32()
+        lib.zkl_synth_vm_segment_chain(seed, seed + i, log_n, flags, None, None, None, C.byref(w))
+        trace = (F128 * (w.value * (1 << log_n)))()
+        pi = AirPublicInputs()
+        rc = lib.zkl_synth_vm_segment_chain(seed, seed + i, log_n, flags, C.byref(rom0), C.cast(trace, C.c_void_p),
+                                            C.byref(pi), C.byref(w))
+        if rc != 0:
+            raise ZklError(rc, "synth_vm_segment_chain failed")
+        out.append((trace, pi, w.value))
+        rom0 = F128(pi.rom_s_out[0].lo, pi.rom_s_out[0].hi)
+    return out
 
 
 def check_request(width: int, n_rows: int, pi: AirPublicInputs, opts: ProofOptions) -> None:

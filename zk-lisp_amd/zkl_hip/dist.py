@@ -94,6 +94,7 @@ def collect_step_proofs(step_bytes):
             d = parse_step_proof(b)
             d["digest"], d["root_trace"] = step_proof_digest(b)
             d["bytes"] = len(b)
+            d["raw"] = bytes(b)
             steps.append(d)
     steps.sort(key=lambda d: d["segment_index"])
     total = steps[0]["segments_total"] if steps else 0
