@@ -307,6 +307,13 @@ typedef struct {
 int zkl_agg_prove(const uint8_t* const* steps, const size_t* step_lens, uint32_t n_steps,
                   const zkl_agg_options* opts, uint8_t** artifact_out, size_t* artifact_len,
                   uint8_t digest_out[32]);
+/* RecursionArtifactCodec::decode (lib.rs:552-660) + RecursionBackend::verify (lib.rs:346-372)
+ * -> verify_agg_proof (prove.rs:732-791): decodes a ZKLRC1 artifact and verifies the
+ * aggregation proof under ZlAggAir and the artifact's public inputs, accepting proof options
+ * whose conjectured security (estimate_conjectured_security_bits, prove.rs:1177-1195) is at
+ * least min_security_bits.  ZKL_OK, or ZKL_E_INVALID with zkl_hip_last_error(NULL) naming the
+ * failing check.  Host-only. */
+int zkl_agg_verify(const uint8_t* artifact, size_t len, uint32_t min_security_bits);
 /* The aggregation trace of the same batch (build_agg_trace_from_transcripts,
  * agg/trace.rs:155-238): 31 columns x rows, column-major; rows_out receives the row count
  * (a power of two >= 8); out may be NULL to query it. */

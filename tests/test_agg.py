@@ -165,3 +165,38 @@ def test_artifact_hash_is_stable(oracle, z, chain3):
     a1, _ = z.agg_prove(chain3, grind=12)
     a2, _ = z.agg_prove(chain3, grind=12)
     assert hashlib.sha256(a1).digest() == hashlib.sha256(a2).digest()
+
+
+@pytest.mark.parametrize("bits", [128, 64])
+def test_agg_verifier_accepts_and_rejects(oracle, z, chain3, bits):
+    """zkl_agg_verify (verify_agg_proof, prove.rs:732-791): the library's artifact verifies;
+    a flipped byte anywhere in the proof, a changed public input, or a security target above
+    what the options give is rejected."""
+    art, _ = z.agg_prove(chain3, grind=8, min_security_bits=bits)
+    z.agg_verify(art, bits)
+    d = z.parse_agg_artifact(art)
+    head = len(art) - len(d["proof"])
+    import random
+    rng = random.Random(bits)
+    for off in sorted(rng.sample(range(head + 40, len(art)), 12)):
+        bad = bytearray(art)
+        bad[off] ^= 1 << rng.randrange(8)
+        with pytest.raises(z.ZklError):
+            z.agg_verify(bytes(bad), bits)
+    # public inputs: v_units_total (asserted at the last row) and the children root (in the seed)
+    for field_off in (6 + 5 * 32, 6 + 3 * 32):
+        bad = bytearray(art)
+        bad[field_off] ^= 1
+        with pytest.raises(z.ZklError):
+            z.agg_verify(bytes(bad), bits)
+    with pytest.raises(z.ZklError, match="conjectured security"):
+        z.agg_verify(art, 200)
+    with pytest.raises(z.ZklError, match="magic"):
+        z.agg_verify(b"ZKLRC0" + art[6:], bits)
+    with pytest.raises(z.ZklError, match="truncated"):
+        z.agg_verify(art[:-9], bits)
+
+
+def test_agg_verifier_accepts_oracle_artifact(oracle, z, chain3):
+    want_art, _, _ = agg_ref.agg_prove(oracle, chain3, grind=8)
+    z.agg_verify(want_art)

@@ -613,12 +613,14 @@ const Deg kAggDegrees[AGG_TC] = {{1, false}, {2, true}, {1, false}, {1, false}, 
                                  {1, false}, {1, false}, {1, false}, {1, false}, {1, false}, {1, false},
                                  {1, false}, {1, false}, {1, false}, {1, false}, {1, false}, {1, false}};
 
-// evaluate_transition (agg/air.rs:113-274) on base-field frames
-void agg_transition(const fe* c, const fe* nx, fe is_last, fe r[AGG_TC]) {
-  const fe nl = fe_sub(fe_one(), is_last);
-  auto chain = [&](int col) { return fe_mul(nl, fe_sub(nx[col], c[col])); };
+// evaluate_transition (agg/air.rs:113-274); T = f128 on the trace / CE domain, the proof's
+// field E at the out-of-domain point
+template <class T>
+void agg_transition(const T* c, const T* nx, T is_last, T r[AGG_TC]) {
+  const T nl = sub(lift<T>(fe_one()), is_last);
+  auto chain = [&](int col) { return mul(nl, sub(nx[col], c[col])); };
   r[0] = c[C_OK];
-  r[1] = fe_mul(nl, fe_sub(nx[C_V_UNITS_ACC], fe_add(c[C_V_UNITS_ACC], fe_mul(c[C_V_UNITS_CHILD], c[C_SEG_FIRST]))));
+  r[1] = mul(nl, sub(nx[C_V_UNITS_ACC], add(c[C_V_UNITS_ACC], mul(c[C_V_UNITS_CHILD], c[C_SEG_FIRST]))));
   r[2] = c[C_TRACE_ROOT_ERR];
   r[3] = c[C_CONSTRAINT_ROOT_ERR];
   r[4] = chain(C_R);
@@ -628,11 +630,11 @@ void agg_transition(const fe* c, const fe* nx, fe is_last, fe r[AGG_TC]) {
   r[8] = chain(C_V0_SUM);
   r[9] = chain(C_V1_SUM);
   r[10] = chain(C_VNEXT_SUM);
-  r[11] = fe_mul(nl, fe_sub(nx[C_CHILD_COUNT_ACC], fe_add(c[C_CHILD_COUNT_ACC], c[C_SEG_FIRST])));
-  const fe xd = fe_sub(c[C_FRI_X1], c[C_FRI_X0]);
-  r[12] = fe_sub(fe_mul(c[C_FRI_VNEXT], xd), fe_sub(fe_mul(c[C_FRI_V1], fe_sub(c[C_FRI_ALPHA], c[C_FRI_X0])),
-                                                   fe_mul(c[C_FRI_V0], fe_sub(c[C_FRI_ALPHA], c[C_FRI_X1]))));
-  r[13] = fe_sub(c[C_FRI_VNEXT], c[C_FRI_Q1]);
+  r[11] = mul(nl, sub(nx[C_CHILD_COUNT_ACC], add(c[C_CHILD_COUNT_ACC], c[C_SEG_FIRST])));
+  const T xd = sub(c[C_FRI_X1], c[C_FRI_X0]);
+  r[12] = sub(mul(c[C_FRI_VNEXT], xd), sub(mul(c[C_FRI_V1], sub(c[C_FRI_ALPHA], c[C_FRI_X0])),
+                                            mul(c[C_FRI_V0], sub(c[C_FRI_ALPHA], c[C_FRI_X1]))));
+  r[13] = sub(c[C_FRI_VNEXT], c[C_FRI_Q1]);
   r[14] = c[C_COMP_SUM];
   r[15] = c[C_ALPHA_DIV_ZM_SUM];
   r[16] = c[C_MAP_L0_SUM];
@@ -698,7 +700,7 @@ std::vector<uint8_t> prove_air(const std::vector<std::vector<fe>>& trace, const 
     fe tc[AGG_TC];
     for (size_t i = 0; i + 1 < n; i++) {  // one transition exemption: the last row is not checked
       for (size_t c = 0; c < W; c++) { cur[c] = trace[c][i]; nxt[c] = trace[c][i + 1]; }
-      agg_transition(cur.data(), nxt.data(), i == n - 1 ? fe_one() : fe_zero(), tc);
+      agg_transition<fe>(cur.data(), nxt.data(), i == n - 1 ? fe_one() : fe_zero(), tc);
       for (int k = 0; k < AGG_TC; k++)
         if (!fe_is_zero(tc[k]))
           throw AggError("aggregation trace does not satisfy ZlAggAir: transition constraint C" + std::to_string(k) +
@@ -758,7 +760,7 @@ std::vector<uint8_t> prove_air(const std::vector<std::vector<fe>>& trace, const 
       }
       const fe xn = fe_pow64(x, n), xg = fe_sub(x, gl);
       const fe p_last = fe_mul(fe_mul(gl, fe_sub(xn, fe_one())), fe_inv(fe_mul(fe{n, 0}, xg)));
-      agg_transition(cur.data(), nxt.data(), p_last, tc);
+      agg_transition<fe>(cur.data(), nxt.data(), p_last, tc);
       T t = zero<T>();
       for (int k = 0; k < AGG_TC; k++) t = add(t, mulb(alpha[k], tc[k]));
       t = mulb(t, fe_mul(xg, fe_inv(fe_sub(xn, fe_one()))));
@@ -980,6 +982,325 @@ std::vector<uint8_t> prove_air(const std::vector<std::vector<fe>>& trace, const 
   return P.v;
 }
 
+// ------------------------------------------------------------------ verification
+// conjectured security as the reference estimates it (estimate_conjectured_security_bits,
+// prove.rs:1177-1195) for the options a proof records
+uint32_t conjectured_bits(uint32_t queries, uint32_t blowup, uint32_t grind, uint32_t ext) {
+  const uint32_t field = 128 * ext;
+  uint32_t qs = (uint32_t)ilog2(blowup) * queries;
+  if (qs >= 80) qs += grind;
+  return std::min(std::min(field, qs) - 1, 128u);
+}
+
+template <class T> T read_e(Rd& r);
+template <> fe read_e<fe>(Rd& r) { return r.felem(); }
+template <> fe2 read_e<fe2>(Rd& r) { const fe a = r.felem(); return fe2{a, r.felem()}; }
+template <class T> T ext_of(fe2 v);
+template <> fe ext_of<fe>(fe2 v) { return v.a; }
+template <> fe2 ext_of<fe2>(fe2 v) { return v; }
+template <class T> T inv_t(T x);
+template <> fe inv_t<fe>(fe x) { return fe_inv(x); }
+template <> fe2 inv_t<fe2>(fe2 x) { return inv(x); }
+template <class T> bool eq_t(T x, T y);
+template <> bool eq_t<fe>(fe x, fe y) { return fe_eq(x, y); }
+template <> bool eq_t<fe2>(fe2 x, fe2 y) { return fe_eq(x.a, y.a) && fe_eq(x.b, y.b); }
+template <class T> T pow_t(T x, uint64_t e) {
+  T r = lift<T>(fe_one());
+  for (; e; e >>= 1, x = mul(x, x))
+    if (e & 1) r = mul(r, x);
+  return r;
+}
+
+// winter-verifier 0.13.1 [WF-recall] for a ZlAggAir proof over E = T (verify_agg_proof,
+// prove.rs:732-791): transcript replay, out-of-domain identity through the same
+// agg_transition, trace / constraint openings, DEEP, FRI folds, remainder, proof of work
+template <class T>
+std::string verify_air(Rd& r, const AggPi& pi, const zkl_proof_options& o, uint32_t W, unsigned logn, size_t nq_proof) {
+  const Hasher& H = hasher();
+  const size_t n = (size_t)1 << logn, B = o.blowup_factor, N = n * B;
+  size_t max_eval = 0;
+  for (const Deg& d : kAggDegrees) max_eval = std::max(max_eval, (size_t)d.base * (n - 1) + (d.cycle ? n - 1 : 0));
+  const size_t Cc = std::max<size_t>(1, (max_eval - (n - 1) + n - 1) / n);
+  const size_t rem_max = (size_t)(o.fri_remainder_max_degree + 1) * B;
+  int nl = 0;
+  for (size_t d = N; d > rem_max; d /= 2) nl++;
+  fe troot, croot, rem_commit;
+  std::vector<fe> fri_roots(nl);
+  {
+    Rd cm = r.vec();
+    troot = cm.digest();
+    croot = cm.digest();
+    for (auto& x : fri_roots) x = cm.digest();
+    rem_commit = cm.digest();
+    if (!cm.done() || r.bad) return "malformed commitments";
+  }
+  std::vector<fe> seed = context_elements(W, n, o);
+  const std::vector<fe> pe = agg_pi_elements(pi);
+  seed.insert(seed.end(), pe.begin(), pe.end());
+  Coin coin{H.hash_elements(seed.data(), seed.size()), 0};
+  auto draw = [&]() -> T { return lift<T>(coin.draw()); };  // draw::<E>: (value, 0)
+  coin.reseed(troot);
+  std::vector<T> alpha(AGG_TC), beta(5);
+  for (auto& a : alpha) a = draw();
+  for (auto& b : beta) b = draw();
+  coin.reseed(croot);
+  const T z = draw();
+  const fe g = root_of_unity(logn);
+  const T zg = mul(z, lift<T>(g));
+
+  if (r.usize() != 1) return "trace queries: exactly one main segment expected";
+  Rd tq_v = r.vec(), tq_p = r.vec(), cq_v = r.vec(), cq_p = r.vec(), ood_ts = r.vec(), ood_es = r.vec();
+  if (r.bad) return "malformed query / OOD sections";
+  const size_t es = sizeof(T) / sizeof(fe) * 16;  // bytes per element of E
+  if (ood_ts.len != 2 * W * es || ood_es.len != 2 * Cc * es) return "OOD frame has the wrong shape";
+  std::vector<T> tz(W), tzg(W), hz(Cc), hzg(Cc);
+  for (auto& v : tz) v = read_e<T>(ood_ts);
+  for (auto& v : tzg) v = read_e<T>(ood_ts);
+  for (auto& v : hz) v = read_e<T>(ood_es);
+  for (auto& v : hzg) v = read_e<T>(ood_es);
+  if (ood_ts.bad || ood_es.bad) return "non-canonical OOD values";
+  {  // H(z) = sum_j H_j(z) z^(j n) against the transition and boundary compositions at z
+    const T zn = pow_t(z, n), gl = lift<T>(fe_pow64(g, n - 1));
+    const T p_last = mul(mul(gl, sub(zn, lift<T>(fe_one()))), inv_t(mul(lift<T>(fe{n, 0}), sub(z, gl))));
+    T tc[AGG_TC];
+    agg_transition<T>(tz.data(), tzg.data(), p_last, tc);
+    T t = zero<T>();
+    for (int k = 0; k < AGG_TC; k++) t = add(t, mul(alpha[k], tc[k]));
+    t = mul(t, mul(sub(z, gl), inv_t(sub(zn, lift<T>(fe_one())))));
+    const size_t cols[5] = {C_OK, C_V_UNITS_ACC, C_CHILD_COUNT_ACC, C_V_UNITS_ACC, C_CHILD_COUNT_ACC};
+    const size_t steps[5] = {0, 0, 0, n - 1, n - 1};
+    const fe vals[5] = {fe_zero(), fe_zero(), fe_zero(), fe{pi.v_units_total, 0}, fe{pi.children_count, 0}};
+    for (int a = 0; a < 5; a++)
+      t = add(t, mul(beta[a], mul(sub(tz[cols[a]], lift<T>(vals[a])), inv_t(sub(z, lift<T>(fe_pow64(g, steps[a])))))));
+    T h = zero<T>(), zj = lift<T>(fe_one());
+    for (size_t j = 0; j < Cc; j++) { h = add(h, mul(hz[j], zj)); zj = mul(zj, zn); }
+    if (!eq_t(h, t)) return "out-of-domain constraint identity does not hold";
+  }
+  {
+    std::vector<fe> oc;
+    for (auto& v : tz) flat(oc, v);
+    for (auto& v : hz) flat(oc, v);
+    for (auto& v : tzg) flat(oc, v);
+    for (auto& v : hzg) flat(oc, v);
+    coin.reseed(H.hash_elements(oc.data(), oc.size()));
+  }
+  std::vector<T> gam(W + Cc);
+  for (auto& c : gam) c = draw();
+  std::vector<T> falpha(nl);
+  for (int d = 0; d < nl; d++) { coin.reseed(fri_roots[d]); falpha[d] = draw(); }
+  coin.reseed(rem_commit);
+  // FRI layer sections, remainder, PoW nonce
+  if ((int)r.usize() != nl) return "FRI layer count mismatch";
+  std::vector<Rd> fl_v(nl), fl_p(nl);
+  for (int d = 0; d < nl; d++) { fl_v[d] = r.vec(); fl_p[d] = r.vec(); }
+  Rd remv = r.vec();
+  if (r.u8() != 0) return "FRI remainder partitions must be 1";
+  const uint64_t nonce = r.u64();
+  if (!r.done()) return "malformed FRI section or trailing bytes";
+  {
+    const fe d = H.merge_with_int(coin.seed, nonce);
+    const uint32_t tzb = d.lo ? (uint32_t)__builtin_ctzll(d.lo) : 64u;
+    if (tzb < o.grinding_factor) return "proof-of-work nonce does not meet the grinding factor";
+  }
+  coin.seed = H.merge_with_int(coin.seed, nonce);
+  coin.counter = 0;
+  std::vector<size_t> pos;
+  for (uint32_t k = 0; k < o.num_queries; k++) pos.push_back((size_t)(coin.draw().lo & (N - 1)));
+  std::sort(pos.begin(), pos.end());
+  pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
+  const size_t nq = pos.size();
+  if (nq != nq_proof) return "num_unique_queries does not match the drawn positions";
+  // openings
+  if (tq_v.len != nq * W * 16 || cq_v.len != nq * Cc * es) return "query value sections have the wrong size";
+  std::vector<fe> trows(nq * W);
+  std::vector<T> crows(nq * Cc);
+  for (auto& v : trows) v = tq_v.felem();
+  for (auto& v : crows) v = read_e<T>(cq_v);
+  if (tq_v.bad || cq_v.bad) return "non-canonical query values";
+  {
+    std::vector<fe> leaves(nq), row;
+    fe root;
+    for (size_t k = 0; k < nq; k++) leaves[k] = H.hash_elements(&trows[k * W], W);
+    if (!batch_merkle_root(tq_p, N, pos, leaves, &root) || !fe_eq(root, troot) || !tq_p.done())
+      return "trace Merkle opening does not reproduce the trace commitment";
+    for (size_t k = 0; k < nq; k++) {
+      row.clear();
+      for (size_t j = 0; j < Cc; j++) flat(row, crows[k * Cc + j]);
+      leaves[k] = H.hash_elements(row.data(), row.size());
+    }
+    if (!batch_merkle_root(cq_p, N, pos, leaves, &root) || !fe_eq(root, croot) || !cq_p.done())
+      return "constraint Merkle opening does not reproduce the constraint commitment";
+  }
+  // DEEP values at the query positions
+  const fe wN = root_of_unity((unsigned)ilog2(N)), three{3, 0};
+  std::vector<T> ev(nq);
+  for (size_t k = 0; k < nq; k++) {
+    const T x = lift<T>(fe_mul(three, fe_pow64(wN, pos[k])));
+    const T iz = inv_t(sub(x, z)), izg = inv_t(sub(x, zg));
+    T y = zero<T>();
+    for (size_t c = 0; c < W; c++) {
+      const T t = lift<T>(trows[k * W + c]);
+      y = add(y, mul(gam[c], add(mul(sub(t, tz[c]), iz), mul(sub(t, tzg[c]), izg))));
+    }
+    for (size_t j = 0; j < Cc; j++) {
+      const T h = crows[k * Cc + j];
+      y = add(y, mul(gam[W + j], add(mul(sub(h, hz[j]), iz), mul(sub(h, hzg[j]), izg))));
+    }
+    ev[k] = y;
+  }
+  // FRI
+  std::vector<size_t> fpos = pos;
+  size_t Nd = N;
+  for (int d = 0; d < nl; d++) {
+    const size_t h = Nd / 2;
+    std::vector<size_t> np;
+    for (size_t p : fpos)
+      if (std::find(np.begin(), np.end(), p % h) == np.end()) np.push_back(p % h);
+    const size_t m = np.size();
+    if (fl_v[d].len != 2 * m * es) return "FRI layer values have the wrong size";
+    std::vector<T> lv(2 * m);
+    for (auto& v : lv) v = read_e<T>(fl_v[d]);
+    if (fl_v[d].bad) return "non-canonical FRI layer values";
+    for (size_t k = 0; k < fpos.size(); k++) {
+      const size_t j = (size_t)(std::find(np.begin(), np.end(), fpos[k] % h) - np.begin());
+      if (!eq_t(lv[2 * j + (fpos[k] >= h ? 1 : 0)], ev[k])) return "FRI layer opening disagrees with the folded values";
+    }
+    {
+      std::vector<size_t> sp(np);
+      std::sort(sp.begin(), sp.end());
+      std::vector<fe> sl(m), row;
+      for (size_t k = 0; k < m; k++) {
+        const size_t j = (size_t)(std::find(np.begin(), np.end(), sp[k]) - np.begin());
+        row.clear();
+        flat(row, lv[2 * j]);
+        flat(row, lv[2 * j + 1]);
+        sl[k] = H.hash_elements(row.data(), row.size());
+      }
+      fe root;
+      if (!batch_merkle_root(fl_p[d], h, sp, sl, &root) || !fe_eq(root, fri_roots[d]) || !fl_p[d].done())
+        return "FRI layer Merkle opening does not reproduce the layer commitment";
+    }
+    const fe gd = root_of_unity((unsigned)ilog2(Nd));
+    std::vector<T> next(m);
+    for (size_t j = 0; j < m; j++) {
+      const fe x0 = fe_mul(three, fe_pow64(gd, np[j])), x1 = fe_sub(fe_zero(), x0);
+      const T num = sub(mul(lv[2 * j + 1], sub(falpha[d], lift<T>(x0))), mul(lv[2 * j], sub(falpha[d], lift<T>(x1))));
+      next[j] = mulb(num, fe_inv(fe_sub(x1, x0)));
+    }
+    fpos = np;
+    ev.swap(next);
+    Nd = h;
+  }
+  const size_t rlen = o.fri_remainder_max_degree + 1;
+  if (remv.len != rlen * es) return "FRI remainder has the wrong size";
+  std::vector<T> rem(rlen);
+  for (auto& v : rem) v = read_e<T>(remv);
+  if (remv.bad) return "non-canonical remainder";
+  {
+    std::vector<fe> rf;
+    for (auto& v : rem) flat(rf, v);
+    if (!fe_eq(H.hash_elements(rf.data(), rf.size()), rem_commit)) return "remainder does not match its commitment";
+  }
+  const fe gr = root_of_unity((unsigned)ilog2(Nd));
+  for (size_t k = 0; k < fpos.size(); k++) {
+    const T x = lift<T>(fe_mul(three, fe_pow64(gr, fpos[k])));
+    T v = zero<T>();
+    for (size_t c = 0; c < rlen; c++) v = add(mul(v, x), rem[c]);
+    if (!eq_t(v, ev[k])) return "FRI remainder does not match the last layer";
+  }
+  return "";
+}
+
+// RecursionArtifactCodec::decode (lib.rs:552-660)
+struct Rdb {
+  const uint8_t* p;
+  size_t n, off = 0;
+  const uint8_t* take(size_t k, const char* what) {
+    if (off + k > n) throw AggError(what);
+    off += k;
+    return p + off - k;
+  }
+  template <class U> U num(const char* what) { U v; memcpy(&v, take(sizeof(U), what), sizeof(U)); return v; }
+};
+AggPi decode_artifact(const uint8_t* b, size_t n, const uint8_t** proof, size_t* plen) {
+  Rdb r{b, n};
+  if (n < 6 || memcmp(b, "ZKLRC1", 6)) throw AggError("invalid recursion artifact magic");
+  r.off = 6;
+  AggPi p;
+  memcpy(p.program_id, r.take(32, "program_id truncated"), 32);
+  memcpy(p.program_commitment, r.take(32, "program_commitment truncated"), 32);
+  memcpy(p.pi_digest, r.take(32, "pi_digest truncated"), 32);
+  memcpy(p.children_root, r.take(32, "children_root truncated"), 32);
+  memcpy(p.batch_id, r.take(32, "batch_id truncated"), 32);
+  p.v_units_total = r.num<uint64_t>("v_units_total truncated");
+  p.children_count = r.num<uint32_t>("children_count truncated");
+  p.m = r.num<uint32_t>("u32 truncated");
+  p.rho = r.num<uint16_t>("u16 truncated");
+  p.q = r.num<uint16_t>("u16 truncated");
+  p.o = r.num<uint16_t>("u16 truncated");
+  p.lambda = r.num<uint16_t>("u16 truncated");
+  p.pi_len = r.num<uint32_t>("u32 truncated");
+  p.v_units = r.num<uint64_t>("v_units(meta) truncated");
+  p.lde_blowup = r.num<uint32_t>("u32 truncated");
+  p.folding_factor = r.num<uint8_t>("u8 truncated");
+  p.redundancy = r.num<uint8_t>("u8 truncated");
+  p.num_layers = r.num<uint8_t>("u8 truncated");
+  p.num_queries = r.num<uint16_t>("u16 truncated");
+  p.grinding_factor = r.num<uint32_t>("u32 truncated");
+  memcpy(p.suite_id, r.take(32, "suite_id truncated"), 32);
+  const uint32_t nms = r.num<uint32_t>("children_ms length truncated");
+  if ((size_t)nms * 4 > n) throw AggError("children_ms truncated");
+  for (uint32_t i = 0; i < nms; i++) p.children_ms.push_back(r.num<uint32_t>("children_ms truncated"));
+  for (uint8_t* x : {p.vm_state_initial, p.vm_state_final, p.ram_u_initial, p.ram_u_final, p.ram_s_initial,
+                     p.ram_s_final})
+    memcpy(x, r.take(32, "boundary state truncated"), 32);
+  for (int i = 0; i < 3; i++) memcpy(p.rom_initial[i], r.take(32, "rom_s_initial truncated"), 32);
+  for (int i = 0; i < 3; i++) memcpy(p.rom_final[i], r.take(32, "rom_s_final truncated"), 32);
+  const uint32_t pl = r.num<uint32_t>("proof length truncated");
+  *proof = r.take(pl, "proof bytes truncated");
+  *plen = pl;
+  return p;
+}
+
+std::string verify_artifact(const uint8_t* art, size_t len, uint32_t min_bits) {
+  const uint8_t* pb;
+  size_t plen;
+  const AggPi pi = decode_artifact(art, len, &pb, &plen);
+  Rd r{pb, plen, 0, false};
+  const uint32_t W = r.u8();
+  if (r.u8() != 0 || r.u8() != 0) return "trace info: auxiliary segments are not supported";
+  const unsigned logn = r.u8();
+  if (r.u8() != 0 || r.u8() != 0) return "trace info: trace metadata must be empty";
+  if (r.u8() != 16) return "context: field element size must be 16";
+  if (r.off + 16 > r.len) return "truncated context";
+  {
+    uint64_t m[2];
+    memcpy(m, r.p + r.off, 16);
+    if (m[0] != P_LO || m[1] != P_HI) return "field modulus in the context is not f128";
+    r.off += 16;
+  }
+  zkl_proof_options o{};
+  o.num_queries = r.u8(); o.blowup_factor = r.u8(); o.grinding_factor = r.u8();
+  o.field_extension = r.u8(); o.fri_folding_factor = r.u8(); o.fri_remainder_max_degree = r.u8();
+  o.batching_constraints = r.u8(); o.batching_deep = r.u8();
+  o.num_partitions = r.u8(); o.hash_rate = r.u8();
+  const size_t nq = r.u8();
+  if (r.bad) return "truncated context";
+  if (W != AGG_W) return "aggregation trace width must be 31 (AggColumns)";
+  if (logn < 3 || logn > 13) return "aggregation trace length out of range";
+  uint32_t np, rate;
+  zkl_select_partitions(W, 1u << logn, &np, &rate);
+  if (o.fri_folding_factor != 2 || o.fri_remainder_max_degree != 1 || o.batching_constraints || o.batching_deep ||
+      o.num_partitions != np || o.hash_rate != rate || o.blowup_factor < 2 || (o.blowup_factor & (o.blowup_factor - 1)) ||
+      o.num_queries == 0)
+    return "unsupported aggregation proof options";
+  if (o.field_extension != 1 && o.field_extension != 2) return "unsupported field extension";
+  // AcceptableOptions::MinConjecturedSecurity(min_bits) (prove.rs:738)
+  if (conjectured_bits(o.num_queries, o.blowup_factor, o.grinding_factor, o.field_extension) < min_bits)
+    return "aggregation proof does not meet the requested conjectured security";
+  return o.field_extension == 2 ? verify_air<fe2>(r, pi, o, W, logn, nq) : verify_air<fe>(r, pi, o, W, logn, nq);
+}
+
 }  // namespace
 }  // namespace zkl
 
@@ -1020,12 +1341,8 @@ int zkl_agg_prove(const uint8_t* const* steps, const size_t* step_lens, uint32_t
     AggOpts ao{std::max<uint32_t>(opts->queries, 16), opts->blowup, opts->grind,
                opts->min_security_bits >= 128 ? 2u : 1u};
     if (ao.queries > 255) throw AggError("queries must be at most 255");
-    if (opts->min_security_bits >= 64) {  // estimate_conjectured_security_bits (prove.rs:1177-1195)
-      const uint32_t field = 128 * (ao.field_ext == 2 ? 2 : 1);
-      uint32_t qs = (uint32_t)ilog2(ao.blowup) * ao.queries;
-      if (qs >= 80) qs += ao.grind;
-      const uint32_t bits = std::min(std::min(field, qs) - 1, 128u);
-      if (bits < opts->min_security_bits)
+    if (opts->min_security_bits >= 64) {  // prove.rs:664-681
+      if (conjectured_bits(ao.queries, ao.blowup, ao.grind, ao.field_ext) < opts->min_security_bits)
         throw AggError(
             "aggregation prover options do not achieve requested min_security_bits; increase --queries/--blowup/--grind "
             "or lower --security-bits");
@@ -1042,6 +1359,14 @@ int zkl_agg_prove(const uint8_t* const* steps, const size_t* step_lens, uint32_t
   memcpy(*artifact_out, art.data(), art.size());
   *artifact_len = art.size();
   return ZKL_OK;
+}
+
+int zkl_agg_verify(const uint8_t* artifact, size_t len, uint32_t min_security_bits) {
+  if (!artifact) return ZKL_E_INVALID;
+  return guarded_call([&] {
+    const std::string e = verify_artifact(artifact, len, min_security_bits);
+    if (!e.empty()) throw AggError(e);
+  });
 }
 
 int zkl_agg_trace(const uint8_t* const* steps, const size_t* step_lens, uint32_t n_steps, zkl_f128* out,

@@ -17,7 +17,7 @@ __all__ = [
     "select_partitions_for_trace", "proof_options", "synth_vm_segment", "STAGE_NAMES",
     "FM_VM", "FM_VM_EXPECT", "FM_POSEIDON", "FM_SPONGE", "FM_MERKLE", "FM_RAM",
     "VmArg", "StepInfo", "check_request", "row_digest_rule", "verify_segment", "step_proof_encode", "step_proof_digest", "parse_step_proof", "children_root",
-    "AggOptions", "agg_prove", "agg_trace", "parse_agg_artifact", "synth_segment_chain", "synth_vm_segment_chain",
+    "AggOptions", "agg_prove", "agg_verify", "agg_trace", "parse_agg_artifact", "synth_segment_chain", "synth_vm_segment_chain",
     "step_info_for",
 ]
 
@@ -157,6 +157,7 @@ def load_library():
                                                P(AirPublicInputs), P(C.c_uint32)]
     lib.zkl_agg_prove.argtypes = [P(C.c_char_p), P(C.c_size_t), C.c_uint32, P(AggOptions), P(P(C.c_uint8)),
                                   P(C.c_size_t), C.c_void_p]
+    lib.zkl_agg_verify.argtypes = [C.c_char_p, C.c_size_t, C.c_uint32]
     lib.zkl_agg_trace.argtypes = [P(C.c_char_p), P(C.c_size_t), C.c_uint32, C.c_void_p, C.c_uint32, P(C.c_uint32)]
     _lib = lib
     return lib
@@ -187,6 +188,15 @@ def agg_prove(steps, queries=64, blowup=16, grind=16, min_security_bits=128):
     data = C.string_at(out, ln.value)
     lib.zkl_hip_free(out)
     return data, bytes(dg)
+
+
+def agg_verify(artifact: bytes, min_security_bits: int = 128) -> None:
+    """RecursionArtifactCodec::decode + RecursionBackend::verify (verify_agg_proof, prove.rs:732-791)
+    of a ZKLRC1 artifact; raises ZklError naming the failing check."""
+    lib = load_library()
+    rc = lib.zkl_agg_verify(bytes(artifact), len(artifact), min_security_bits)
+    if rc:
+        raise ZklError(rc, lib.zkl_hip_last_error(None).decode(errors="replace"))
 
 
 def agg_trace(steps):
