@@ -459,8 +459,8 @@ def agg_trace(ol, p, steps, txs):
     """build_agg_trace_from_transcripts (agg/trace.rs:155-693) for an honest batch: every
     opening of every child reproduces its commitment (the root errors are zero)."""
     nc = len(steps)
-    rows = 8
-    while rows < nc:
+    rows = 8  # next_pow2(max(children, 8)) (agg/trace.rs:396-405), keeping one padding row so
+    while rows < nc + 1:  # the last-row assertions (agg/air.rs:276-304) can hold (DESIGN.md §10)
         rows *= 2
     T = [[0] * rows for _ in range(NCOLS)]
     wc = Coin(ol, agg_pi_elements(p) + [0xA9])  # derive_agg_fs_weights (agg/trace.rs:95-125)
@@ -592,6 +592,9 @@ def prove_agg(ol, T, p, queries, blowup, grind, ext):
     for i in range(n - 1):  # the trace satisfies the AIR (winterfell's debug validation)
         tc = agg_transition([T[c][i] for c in range(Wd)], [T[c][i + 1] for c in range(Wd)], 0)
         assert not any(tc), f"aggregation trace does not satisfy ZlAggAir (row {i})"
+    assert T[OK][0] == 0 and T[VACC][0] == 0 and T[CNT][0] == 0, "aggregation trace assertion fails"
+    assert T[VACC][n - 1] == p["v_units_total"] and T[CNT][n - 1] == p["children_count"], \
+        "aggregation trace assertion fails"
     logn = n.bit_length() - 1
     N = n * blowup
     parts, rate = 1, 8 if Wd <= 32 else 16  # select_partitions_for_trace (utils.rs:394-409)

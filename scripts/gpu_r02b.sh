@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 GPU pass: GPU test suite, default bench line, 2-rank launcher rehearsal on one GPU
+# Round-2 GPU pass (after scripts/gpu_tests.sh): default bench line, 2-rank launcher rehearsal on one GPU
 # (configs[3] path incl. the aggregation proof on rank 0), rocprofv3 kernel statistics and the
 # FETCH_SIZE / WRITE_SIZE passes of the current build.  Usage (repo root on the box):
 #   bash scripts/gpu_r02b.sh [tag]     -> gpurun_out/<tag>/
@@ -8,8 +8,6 @@ tag=${1:-r02b}
 root=$PWD
 out=$root/gpurun_out/$tag
 mkdir -p $out
-timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > $out/pytest_gpu.log 2>&1 || { echo "pytest gpu failed rc=$?"; tail -40 $out/pytest_gpu.log; exit 1; }
-tail -3 $out/pytest_gpu.log
 timeout -k 10 900 python bench.py > $out/bench.json 2> $out/bench.err || { echo "bench failed rc=$?"; tail -20 $out/bench.err; exit 1; }
 cat $out/bench.json
 ZKL_BENCH_DEVICE=0 timeout -k 10 900 python bench.py --gpus 2 --steps 3 --warmup 1 --c5-log-n 0 > $out/bench_2rank_1gpu.json 2> $out/bench2.err || { echo "2-rank bench failed rc=$?"; tail -20 $out/bench2.err; exit 1; }

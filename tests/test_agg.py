@@ -87,6 +87,19 @@ def test_aggregation_other_layouts(oracle, z, flags, log_n):
     assert art == want_art and dg == want_dg
 
 
+def test_power_of_two_children_keep_a_padding_row(oracle, z):
+    """8 children: the reference's next_pow2(max(8, 8)) = 8 rows would put the last child's
+    pre-increment accumulators on the asserted last row (agg/air.rs:276-304); the trace keeps
+    one padding row (16 rows) and the batch proves and verifies."""
+    steps = _steps(oracle, z, 8, program=PROGRAM + 0x500, queries=4, grind=0)
+    T = z.agg_trace(steps)
+    assert len(T[0]) == 16 and T[agg_ref.VACC][-1] == 8 * 32 * 4 and T[agg_ref.CNT][-1] == 8
+    art, dg = z.agg_prove(steps, grind=8)
+    want_art, want_dg, _ = agg_ref.agg_prove(oracle, steps, grind=8)
+    assert art == want_art and dg == want_dg
+    z.agg_verify(art)
+
+
 def test_aggregation_trace_layout(oracle, z, chain3):
     """AggColumns (agg/layout.rs:97-175) on an honest batch: one seg_first row per child,
     accumulators before the increment, zero error columns, the FRI sample satisfies C12/C13."""

@@ -541,8 +541,14 @@ std::vector<std::vector<fe>> build_agg_trace(const AggPi& p, const std::vector<C
   }
   if (vsum != p.v_units_total) throw AggError("AggAirPublicInputs.v_units_total must equal sum of child meta.v_units");
 
+  // rows: next_pow2(max(children, 8)) in the reference (agg/trace.rs:396-405).  With a
+  // power-of-two child count >= 8 that leaves no padding row, and the last row then holds the
+  // last child's accumulators *before* its increment, so the assertions v_units_acc[last] =
+  // v_units_total and child_count_acc[last] = children_count (agg/air.rs:276-304) cannot hold
+  // and no valid aggregation proof exists.  One padding row is always kept here (DESIGN.md
+  // §10); other child counts give the reference's trace length.
   size_t rows = 1;
-  while (rows < std::max(nc, MIN_AGG_TRACE_ROWS)) rows *= 2;
+  while (rows < std::max(nc + 1, MIN_AGG_TRACE_ROWS)) rows *= 2;
   std::vector<std::vector<fe>> T(AGG_W, std::vector<fe>(rows, fe_zero()));
   const fe vm0 = fold_bytes32(p.vm_state_initial), vm1 = fold_bytes32(p.vm_state_final);
   const fe ru0 = fold_bytes32(p.ram_u_initial), ru1 = fold_bytes32(p.ram_u_final);
