@@ -913,8 +913,8 @@ __device__ __forceinline__ fe ntt_canon(const uint32_t l[5]) {
 // otherwise own only half of each 128-byte line they touch (G = ELEMS >> r < 8 consecutive L
 // at a stride S >= G: the other half went to a workgroup on another XCD and the line was
 // fetched twice -- the 8-stage top pass of the trace LDE fetched 7.1 GB for 3.4 GB)
-template <int ELEMS>
-__global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restrict__ data, size_t ncols, int logN, int r,
+template <int ELEMS, int THREADS>
+__global__ __launch_bounds__(THREADS) void ntt_dit_lazy_kernel(fe* __restrict__ data, size_t ncols, int logN, int r,
                                                                   int logS, MontTab roots, const fe* __restrict__ src,
                                                                   int src_logb) {
   constexpr int PITCHED = ELEMS + ELEMS / 16;
@@ -951,7 +951,7 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
     return (col << logN) + ((Hb << logS) << r) + (size_t)t * S + L;
   };
   const size_t Nmask = ((size_t)1 << logN) - 1;
-  for (int e = threadIdx.x; e < ELEMS; e += NTT_THREADS) {
+  for (int e = threadIdx.x; e < ELEMS; e += THREADS) {
     const int g = gfast ? (e % G) : (e >> r);
     const int t = gfast ? (e / G) : (e & (R - 1));
     bool ok;
@@ -991,10 +991,10 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
   // group; stage lh pairs (0,1), (2,3) under one twiddle, stage lh+1 pairs (0,2), (1,3)
   for (; lh + 1 < r; lh += 2) {
     const int h = 1 << lh;
-    constexpr int QPT = ELEMS / 4 / NTT_THREADS;
+    constexpr int QPT = ELEMS / 4 / THREADS;
 #pragma unroll
     for (int i = 0; i < QPT; i++) {
-      const int u = threadIdx.x + NTT_THREADS * i;
+      const int u = threadIdx.x + THREADS * i;
       const int g = u % G;
       const int w = u / G;
       const int k = w & (h - 1);
@@ -1018,10 +1018,10 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
   }
   if (lh < r) {  // odd stage count: one radix-2 stage
     const int h = 1 << lh;
-    constexpr int BPT = ELEMS / 2 / NTT_THREADS;
+    constexpr int BPT = ELEMS / 2 / THREADS;
 #pragma unroll
     for (int i = 0; i < BPT; i++) {
-      const int u = threadIdx.x + NTT_THREADS * i;
+      const int u = threadIdx.x + THREADS * i;
       const int g = u % G;
       const int w = u / G;
       const int k = w & (h - 1);
@@ -1037,7 +1037,7 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_dit_lazy_kernel(fe* __restric
     }
     __syncthreads();
   }
-  for (int e = threadIdx.x; e < ELEMS; e += NTT_THREADS) {
+  for (int e = threadIdx.x; e < ELEMS; e += THREADS) {
     const int g = gfast ? (e % G) : (e >> r);
     const int t = gfast ? (e / G) : (e & (R - 1));
     bool ok;
@@ -1060,6 +1060,17 @@ static bool ntt_lazy_enabled() {
   return v != 0;
 }
 void set_ntt_lazy(bool on) { g_ntt_lazy.store(on ? 1 : 0); }
+// measured (profiles/r02, scripts/ab_ntt_wide.sh): the 2048-element / 256-thread form halves
+// the top pass's fetch (7.1 -> 3.7 GB) but its passes run no faster (fewer waves per CU hide
+// less of the butterfly chains); 2048 elements on 512 threads keeps the waves and gives NTT
+// 8.3 -> 8.0 ms per proof: default 2
+static int ntt_wide_mode() {
+  static const int m = [] {
+    const char* e = getenv("ZKL_NTT_WIDE");
+    return e ? atoi(e) : 2;
+  }();
+  return m;
+}
 
 static int ilog2s(size_t n) { int k = 0; while (((size_t)1 << k) < n) k++; return k; }
 
@@ -1118,14 +1129,19 @@ static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
       size_t groups = (N >> r) * ncols;
       size_t G = NTT_ELEMS >> r;
       if (ntt_lazy_enabled()) {
-        const bool wide = G < 8 && ((size_t)1 << cur) >= G;  // see ntt_dit_lazy_kernel
+        // wide mode (ZKL_NTT_WIDE): 1 = 2048 elements / 256 threads, 2 = 2048 / 512 for the
+        // passes whose 1024-element groups own only half lines (see ntt_dit_lazy_kernel)
+        const int wm = ntt_wide_mode();
+        const bool wide = wm > 0 && G < 8 && ((size_t)1 << cur) >= G;
         const size_t Gw = wide ? 2 * G : G;
         const unsigned grid = (unsigned)((groups + Gw - 1) / Gw);
         const fe* sp = cur == lo ? src : nullptr;
-        if (wide)
-          ntt_dit_lazy_kernel<2 * NTT_ELEMS><<<grid, NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots, sp, src_logb);
+        if (wide && wm == 2)
+          ntt_dit_lazy_kernel<2 * NTT_ELEMS, 2 * NTT_THREADS><<<grid, 2 * NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots, sp, src_logb);
+        else if (wide)
+          ntt_dit_lazy_kernel<2 * NTT_ELEMS, NTT_THREADS><<<grid, NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots, sp, src_logb);
         else
-          ntt_dit_lazy_kernel<NTT_ELEMS><<<grid, NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots, sp, src_logb);
+          ntt_dit_lazy_kernel<NTT_ELEMS, NTT_THREADS><<<grid, NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots, sp, src_logb);
       } else
         ntt_pass_kernel<false><<<(unsigned)((groups + G - 1) / G), NTT_THREADS, 0, s>>>(
             d, ncols, logN, r, cur, roots, logTab, cur == lo ? src : nullptr, src_logb);
