@@ -1316,12 +1316,27 @@ using namespace zkl;
 namespace {
 std::vector<Child> load_children(const uint8_t* const* steps, const size_t* lens, uint32_t n) {
   if (!steps || !lens || n == 0) throw AggError("RecursionBackend::recursion_prove requires at least one step proof");
-  std::vector<Child> ch;
-  ch.reserve(n);
-  for (uint32_t i = 0; i < n; i++) {
+  for (uint32_t i = 0; i < n; i++)
     if (!steps[i]) throw AggError("null step proof");
-    ch.push_back(load_child(steps[i], lens[i]));
-  }
+  // children replay independently (~10^4 host permutations each at 2^16 rows): host threads
+  std::vector<Child> ch(n);
+  std::vector<std::string> err(n);
+  std::atomic<uint32_t> next{0};
+  const unsigned nt = std::max(1u, std::min<unsigned>(std::min(16u, std::thread::hardware_concurrency()), n));
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; t++)
+    th.emplace_back([&] {
+      for (uint32_t i; (i = next.fetch_add(1)) < n;) {
+        try {
+          ch[i] = load_child(steps[i], lens[i]);
+        } catch (const std::exception& e) {
+          err[i] = e.what();
+        }
+      }
+    });
+  for (auto& x : th) x.join();
+  for (uint32_t i = 0; i < n; i++)
+    if (!err[i].empty()) throw AggError("child " + std::to_string(i) + ": " + err[i]);
   for (const Child& c : ch)
     if (memcmp(c.step.suite, ch[0].step.suite, 32))
       throw AggError("RecursionBackend::recursion_prove requires all steps to share the same suite_id");

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <stdexcept>
+#include <thread>
 
 #include "air_eval.h"
 #include "air_host.h"
@@ -249,9 +250,26 @@ std::string verify_segment_ex(const uint8_t* proof, size_t len, const zkl_air_pu
   }
   VCoin coin{H.hash_elements(seed.data(), seed.size()), 0};
   coin.reseed(V.trace_root);
-  std::vector<fe> alphas(air.n_tc), betas(air.assertions.size());
-  for (auto& a : alphas) a = coin.draw();
-  for (auto& b : betas) b = coin.draw();
+  // composition coefficients: draw k = merge_with_int(seed, k), k = 1.. (alphas then betas).
+  // They are independent, so the ~2.9e5 of a 2^16-row segment run on host threads.  The
+  // replay without the out-of-domain identity needs none of them: a reseed follows, and
+  // draws only advance the counter the reseed resets (agg/fs.rs:132-138 skips them too).
+  std::vector<fe> alphas, betas;
+  if (check_ood) {
+    const size_t na = (size_t)air.n_tc, nb = air.assertions.size(), tot = na + nb;
+    std::vector<fe> all(tot);
+    const fe sd = coin.seed;
+    const size_t nt = std::max<size_t>(1, std::min<size_t>(16, std::thread::hardware_concurrency()));
+    const size_t chunk = (tot + nt - 1) / nt;
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < nt && t * chunk < tot; t++)
+      th.emplace_back([&, t] {
+        for (size_t k = t * chunk; k < std::min(tot, (t + 1) * chunk); k++) all[k] = H.merge_with_int(sd, k + 1);
+      });
+    for (auto& x : th) x.join();
+    alphas.assign(all.begin(), all.begin() + (long)na);
+    betas.assign(all.begin() + (long)na, all.end());
+  }
   coin.reseed(V.constraint_root);
   V.z = coin.draw();
   const fe z = V.z, zg = fe_mul(z, g);
