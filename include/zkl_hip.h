@@ -264,6 +264,49 @@ int zkl_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f
 int zkl_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t log_n, uint32_t flags, const zkl_f128* rom0_in,
                                zkl_f128* trace_out, zkl_air_public_inputs* pi_out, uint32_t* width_out);
 
+/* ---- op-list trace builder ------------------------------------------
+ * zk_lisp_compiler::builder::Op (builder.rs:25-158), one op per 32-row level.  Field use:
+ *   CONST dst imm | MOV dst a(=src) | ADD/SUB/MUL/EQ dst a b | NEG dst a | SELECT dst c a b
+ *   ASSERT dst c | ASSERT_BIT, ASSERT_RANGE_LO, ASSERT_RANGE_HI dst c(=r)
+ *   ASSERT_RANGE dst c(=r) bits | DIVMOD dst(=dst_q) dst2(=dst_r) a b
+ *   DIVMOD128 a(=a_hi) c(=a_lo) b dst(=dst_q) dst2(=dst_r) | MULWIDE dst(=dst_lo) dst2(=dst_hi) a b
+ *   LOAD dst a(=addr) | STORE a(=addr) b(=src) | SABSORBN n_regs regs[] | SSQUEEZE dst
+ *   MERKLE_FIRST dst(=leaf_reg) a(=dir_reg) b(=sib_reg) | MERKLE_STEP, MERKLE_LAST a(=dir) b(=sib)
+ *   END
+ * Register indices < 8. */
+enum {
+  ZKL_OP_CONST = 0, ZKL_OP_MOV, ZKL_OP_ADD, ZKL_OP_SUB, ZKL_OP_MUL, ZKL_OP_NEG, ZKL_OP_EQ, ZKL_OP_SELECT,
+  ZKL_OP_ASSERT, ZKL_OP_ASSERT_BIT, ZKL_OP_ASSERT_RANGE, ZKL_OP_ASSERT_RANGE_LO, ZKL_OP_ASSERT_RANGE_HI,
+  ZKL_OP_DIVMOD, ZKL_OP_DIVMOD128, ZKL_OP_MULWIDE, ZKL_OP_LOAD, ZKL_OP_STORE, ZKL_OP_SABSORBN, ZKL_OP_SSQUEEZE,
+  ZKL_OP_MERKLE_FIRST, ZKL_OP_MERKLE_STEP, ZKL_OP_MERKLE_LAST, ZKL_OP_END
+};
+typedef struct {
+  uint32_t kind;
+  uint8_t dst, dst2, a, b, c, bits, n_regs, reserved;
+  uint8_t regs[10];
+  uint64_t imm;
+} zkl_op;
+/* build_full_trace (vm/trace/mod.rs:434-524) of a program: n_rows = 32 * next_pow2(n_ops)
+ * (levels past the last op keep only the schedule gates, pc and domain tags), initial registers
+ * from secret_args (u64, r0..) and main_args flattened into slots in the tail registers
+ * (vm.rs:64-104), the VM, RAM and ROM builders (vm.rs, ram.rs, rom.rs), written in the segment
+ * layout of the features the ops use (sponge ops: FM_SPONGE | FM_POSEIDON, Load / Store:
+ * FM_RAM, Merkle steps: FM_MERKLE | FM_POSEIDON; vm/layout.rs:183-313).  Also the AIR public
+ * inputs prove_segment derives for the whole trace as one segment (prove.rs:292-423; merkle_root
+ * = the accumulator after the last MerkleStepLast).  rom0_in: ROM lane 0 entering the first
+ * level (NULL: 0).  trace_out NULL: only *width_out / *n_rows_out.  ZKL_E_INVALID on a register
+ * index > 7, more than 10 pending absorbs (push_absorb, vm.rs:925-935), more than 8 main-arg
+ * slots, or an unknown kind. */
+int zkl_build_trace(const zkl_op* ops, uint32_t n_ops, const uint8_t program_id[32],
+                    const uint8_t program_commitment[32], const uint64_t* secret_args, uint32_t n_secret,
+                    const zkl_vm_arg* main_args, uint32_t n_main, const zkl_f128* rom0_in, zkl_f128* trace_out,
+                    zkl_air_public_inputs* pi_out, uint32_t* width_out, uint32_t* n_rows_out);
+/* rom_acc_from_program (romacc.rs:22-80): the t=3 ROM accumulator over the ops' virtual map rows
+ * (opcode bit + register selectors, romacc.rs:82-260), next_pow2(n_ops) levels from state 0 —
+ * what the verifier recomputes for pi.rom_acc when the commitment is non-zero (prove.rs:815-821,
+ * lib.rs:210-214).  Equals the trace's rom_acc for a one-segment trace built from rom0 = 0. */
+int zkl_rom_acc_from_program(const zkl_op* ops, uint32_t n_ops, const uint8_t program_id[32], zkl_f128 out[3]);
+
 /* ---- zl1 step proof (host-side, no device work) ----------------------------------
  * StepProof::to_bytes (proof/step.rs:79-151) of the step proof prove_segment builds around
  * an inner proof from zkl_hip_prove_segment*: "ZKLSTP1" | lambda | suite | core pi |

@@ -122,6 +122,11 @@ int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f
 /* ---------------- prover / verifier ---------------- */
 int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t log_n, uint32_t flags, const zkl_f128 *rom0_in,
                                zkl_f128 *trace_out, zkl_air_public_inputs *pi_out, uint32_t *width_out);
+/* op-list trace builder, zkl_build_trace's twin (same arguments; 0 / -1) */
+int orc_build_trace(const zkl_op *ops, uint32_t n_ops, const uint8_t program_id[32], const uint8_t commitment[32],
+                    const uint64_t *secret_args, uint32_t n_secret, const zkl_vm_arg *main_args, uint32_t n_main,
+                    const zkl_f128 *rom0_in, zkl_f128 *trace_out, zkl_air_public_inputs *pi_out, uint32_t *width_out,
+                    uint32_t *n_rows_out);
 int orc_prove_segment(const zkl_f128 *trace, uint32_t width, uint32_t n,
                       const zkl_air_public_inputs *pi, const zkl_proof_options *opts,
                       uint8_t **proof, size_t *len, int boundary_mode);

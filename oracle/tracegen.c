@@ -30,9 +30,12 @@ static uint64_t splitmix64(uint64_t *s) {
   return z ^ (z >> 31);
 }
 
-enum { OP_CONST = 0, OP_MOV = 1, OP_ADD = 2, OP_SUB = 3, OP_MUL = 4, OP_NEG = 5, OP_ABSORB = 10, OP_SQUEEZE = 11,
-       OP_CADDR = 12, OP_LOAD = 15, OP_STORE = 16, OP_MFIRST = 20, OP_MSTEP = 21, OP_MLAST = 22, OP_END = 99 };
-typedef struct { int kind; int dst, a, b; uint64_t imm; int nabs; int abs_regs[3]; } synth_op;
+enum { OP_CONST = 0, OP_MOV = 1, OP_ADD = 2, OP_SUB = 3, OP_MUL = 4, OP_NEG = 5, OP_EQ = 6, OP_SELECT = 7,
+       OP_ASSERT = 9, OP_ASSERT_BIT = 10, OP_RANGE = 11, OP_DIVMOD = 12, OP_DIV128 = 13, OP_MULWIDE = 14,
+       OP_ABSORB = 30, OP_SQUEEZE = 31, OP_CADDR = 32, OP_RANGE_LO = 33, OP_RANGE_HI = 34,
+       OP_LOAD = 15, OP_STORE = 16, OP_MFIRST = 20, OP_MSTEP = 21, OP_MLAST = 22, OP_END = 99, OP_PAD = 100 };
+/* dst2: DivMod r / DivMod128 r / MulWide hi; c: Select / Assert* / AssertRange* register, DivMod128 a_lo */
+typedef struct { int kind; int dst, a, b; uint64_t imm; int nabs; int abs_regs[10]; int c, dst2, bits; } synth_op;
 
 #define SYN_SPONGE 1u
 #define SYN_RAM 2u
@@ -83,8 +86,9 @@ static void synth_program(uint64_t seed, size_t levels, synth_op *ops, uint32_t 
   }
   if ((flags & SYN_MERKLE) && levels >= 8) {
     uint64_t r = splitmix64(&st);
-    synth_op m[5] = {{OP_CONST, 5, 0, 0, r & 1, 0, {0}}, {OP_CONST, 6, 0, 0, (r >> 1) & 1, 0, {0}},
-                     {OP_MFIRST, 0, 5, 1, 0, 0, {0}}, {OP_MSTEP, 0, 6, 2, 0, 0, {0}}, {OP_MLAST, 0, 5, 3, 0, 0, {0}}};
+    synth_op m[5] = {{OP_CONST, 5, 0, 0, r & 1, 0, {0}, 0, 0, 0}, {OP_CONST, 6, 0, 0, (r >> 1) & 1, 0, {0}, 0, 0, 0},
+                     {OP_MFIRST, 0, 5, 1, 0, 0, {0}, 0, 0, 0}, {OP_MSTEP, 0, 6, 2, 0, 0, {0}, 0, 0, 0},
+                     {OP_MLAST, 0, 5, 3, 0, 0, {0}, 0, 0, 0}};
     for (int i = 0; i < 5; i++) ops[1 + i] = m[i]; /* MerkleStep*: dst = leaf reg, a = dir reg, b = sib reg */
   }
   memset(&ops[levels - 1], 0, sizeof ops[levels - 1]);
@@ -240,31 +244,19 @@ int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f
   return orc_synth_vm_segment_chain(seed, seed, log_n, flags, NULL, t, pi, width_out);
 }
 
-/* the same with ROM lane 0 entering the first level at *rom0_in (the accumulator lane the
- * aggregation chains across segments, agg/trace.rs:524-541) instead of 0 */
-int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t log_n, uint32_t flags, const zkl_f128 *rom0_in, zkl_f128 *t,
-                               zkl_air_public_inputs *pi, uint32_t *width_out) {
-  if (log_n < 5 || log_n > 26 || (flags & ~7u)) return -1;
-  if ((flags & SYN_MERKLE) && log_n < 8) return -1;
-  size_t n = (size_t)1 << log_n, levels = n / 32;
+/* The trace of a program of `levels` ops (OP_PAD past its last op) and its AIR public inputs:
+ * build_full_trace (mod.rs:434-524) with the initial registers regs0 (vm.rs:64-104), ROM lane 0
+ * entering the first level = rom0, written in the segment layout of the features. */
+static int build_core(const synth_op *ops, size_t levels, const uint8_t pid[32], const uint8_t commit[32], int sponge,
+                      int ram, int merkle, fe rom0, const fe regs0[NR], const fe *slots, uint32_t n_slots, zkl_f128 *t,
+                      zkl_air_public_inputs *pi) {
+  size_t n = levels * 32;
   zk_cols c;
-  cols_for_config(1, !!(flags & SYN_RAM), 0, !!(flags & SYN_MERKLE), 1, &c);
-  if (width_out) *width_out = (uint32_t)c.width;
-  if (!t) return 0;
+  cols_for_config(1, ram, sponge, merkle, 1, &c);
   memset(t, 0, (size_t)c.width * n * sizeof(zkl_f128));
   memset(pi, 0, sizeof *pi);
-
-  char desc[160];
-  snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 %s%s%sseed=0x%016llx levels=%zu",
-           (flags & SYN_SPONGE) ? "sponge " : "", (flags & SYN_RAM) ? "ram " : "", (flags & SYN_MERKLE) ? "merkle " : "",
-           (unsigned long long)program_seed, levels);
-  uint8_t pid[32];
-  orc_blake3((const uint8_t *)desc, strlen(desc), pid);
   pos_suite ps;
   pos_suite_derive(pid, POS_ROUNDS, &ps);
-
-  synth_op *ops = (synth_op *)malloc(levels * sizeof(synth_op));
-  synth_program(seed, levels, ops, flags);
 
   /* build_empty_trace + pc + dom tags (mod.rs:386-470) */
   for (size_t l = 0; l < levels; l++) {
@@ -277,7 +269,8 @@ int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t lo
     set_fe(t, n, c.lanes_start + 11, b, ps.dom[1]);
   }
   /* VmTraceBuilder (vm.rs:58-888) */
-  fe regs[NR] = {0};
+  fe regs[NR];
+  memcpy(regs, regs0, sizeof regs);
   int pending[10], npending = 0;
   /* RAM: host memory (addr -> value) and the event log (addr, clk, val, is_write) */
   size_t n_ev = 0, n_mem = 0;
@@ -288,8 +281,9 @@ int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t lo
     fe next[NR];
     memcpy(next, regs, sizeof next);
     size_t b = l * 32, rm = b, rf = b + 28;
-    if (l == 0) set_fe(t, n, c.pi_prog, 0, be_from_le8(pid));
     const synth_op *op = &ops[l];
+    if (op->kind == OP_PAD) continue; /* registers stay zero past the program (build_empty_trace) */
+    if (l == 0) set_fe(t, n, c.pi_prog, 0, be_from_le8(pid));
     int onehot = -1;
     switch (op->kind) {
       case OP_CONST: onehot = 0; break;
@@ -298,6 +292,16 @@ int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t lo
       case OP_SUB: onehot = 3; break;
       case OP_MUL: onehot = 4; break;
       case OP_NEG: onehot = 5; break;
+      case OP_EQ: onehot = 6; break;
+      case OP_SELECT: onehot = 7; break;
+      case OP_ASSERT: onehot = 9; break;
+      case OP_ASSERT_BIT: onehot = 10; break;
+      case OP_RANGE:
+      case OP_RANGE_LO:
+      case OP_RANGE_HI: onehot = 11; break;
+      case OP_DIVMOD: onehot = 12; break;
+      case OP_DIV128: onehot = 13; break;
+      case OP_MULWIDE: onehot = 14; break;
       case OP_ABSORB:
       case OP_SQUEEZE: onehot = 8; break;
       case OP_CADDR: onehot = 0; break;
@@ -312,7 +316,11 @@ int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t lo
       /* SAbsorbN / SSqueeze (vm.rs:565-672): op_sponge and lane selectors at map and final */
       int sel_regs[10], k = 0;
       if (op->kind == OP_ABSORB) {
-        for (int i = 0; i < op->nabs; i++) { sel_regs[k++] = op->abs_regs[i]; pending[npending++] = op->abs_regs[i]; }
+        for (int i = 0; i < op->nabs; i++) {
+          if (npending == 10) { free(ev); free(mem); return -1; } /* push_absorb overflow (vm.rs:925-935) */
+          sel_regs[k++] = op->abs_regs[i];
+          pending[npending++] = op->abs_regs[i];
+        }
       } else {
         for (int i = 0; i < npending; i++) sel_regs[k++] = pending[i];
       }
@@ -377,23 +385,91 @@ int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t lo
       ev[n_ev][0] = addr; ev[n_ev][1] = (fe)l; ev[n_ev][2] = val; ev[n_ev][3] = op->kind == OP_STORE;
       n_ev++;
     }
-    for (int q = 0; q < 2 && onehot >= 0 && onehot != 8 && onehot < 15; q++) {
-      size_t row = rows[q];
-      set_fe(t, n, c.op[onehot], row, 1);
-      set_sel(t, n, row, c.sel_dst0, op->dst);
-      if (op->kind == OP_CONST || op->kind == OP_CADDR) set_fe(t, n, c.imm, row, (fe)op->imm);
-      else set_sel(t, n, row, c.sel_a, op->a);
-      if (op->kind == OP_ADD || op->kind == OP_SUB || op->kind == OP_MUL) set_sel(t, n, row, c.sel_b, op->b);
-    }
-    switch (op->kind) {
+    /* ALU ops (vm.rs:199-564): op bit and selectors on map and final rows, imm / eq_inv /
+     * range-gadget witnesses on both rows */
+    const int k_ = op->kind;
+    const fe M64 = (((fe)1) << 64) - 1;
+    fe ra = regs[op->a], rb = regs[op->b], rc = regs[op->c];
+    fe imm = 0, inv = 0, bitv[32];
+    int gadget = 0;
+    switch (k_) {
       case OP_CONST:
-      case OP_CADDR: next[op->dst] = (fe)op->imm; break;
-      case OP_MOV: next[op->dst] = regs[op->a]; break;
-      case OP_ADD: next[op->dst] = fe_add(regs[op->a], regs[op->b]); break;
-      case OP_SUB: next[op->dst] = fe_sub(regs[op->a], regs[op->b]); break;
-      case OP_MUL: next[op->dst] = fe_mul(regs[op->a], regs[op->b]); break;
-      case OP_NEG: next[op->dst] = fe_neg(regs[op->a]); break;
+      case OP_CADDR: imm = (fe)op->imm; next[op->dst] = imm; break;
+      case OP_MOV: next[op->dst] = ra; break;
+      case OP_ADD: next[op->dst] = fe_add(ra, rb); break;
+      case OP_SUB: next[op->dst] = fe_sub(ra, rb); break;
+      case OP_MUL: next[op->dst] = fe_mul(ra, rb); break;
+      case OP_NEG: next[op->dst] = fe_neg(ra); break;
+      case OP_EQ: {
+        fe d = fe_sub(ra, rb);
+        inv = d ? fe_inv(d) : 0;
+        next[op->dst] = d ? 0 : 1;
+        break;
+      }
+      case OP_SELECT: next[op->dst] = fe_add(fe_mul(rc, ra), fe_mul(fe_sub(1, rc), rb)); break;
+      case OP_ASSERT:
+      case OP_ASSERT_BIT: next[op->dst] = 1; break;
+      case OP_RANGE: { /* 32-bit form: imm 1, eq_inv 0, the low min(bits, 32) bits of r */
+        int kb = op->bits < 32 ? op->bits : 32;
+        for (int i = 0; i < 32; i++) bitv[i] = i < kb ? (rc >> i) & 1 : 0;
+        imm = 1; gadget = 1;
+        next[op->dst] = 1;
+        break;
+      }
+      case OP_RANGE_LO: /* 64-bit stage 0: imm 0, eq_inv 1, low 32 bits; dst <- r mod 2^32 */
+        for (int i = 0; i < 32; i++) bitv[i] = (rc >> i) & 1;
+        inv = 1; gadget = 1;
+        next[op->dst] = rc & 0xFFFFFFFFu;
+        break;
+      case OP_RANGE_HI: /* stage 1: imm 1, eq_inv 1, bits 32..63 */
+        for (int i = 0; i < 32; i++) bitv[i] = (rc >> (32 + i)) & 1;
+        imm = 1; inv = 1; gadget = 1;
+        next[op->dst] = 1;
+        break;
+      case OP_DIVMOD: { /* canonical values as u128; results mod 2^64; eq_inv = (b mod 2^64)^-1 */
+        fe q = rb ? ra / rb : 0, r = rb ? ra % rb : ra;
+        next[op->dst] = q & M64;
+        next[op->dst2] = r & M64;
+        inv = rb ? fe_inv(rb & M64) : 0;
+        break;
+      }
+      case OP_MULWIDE: {
+        fe prod = (ra & M64) * (rb & M64);
+        next[op->dst] = prod & M64;
+        next[op->dst2] = prod >> 64;
+        break;
+      }
+      case OP_DIV128: { /* ((a_hi << 64) | a_lo mod 2^64) / b; imm = a_lo */
+        fe num = (ra << 64) | (rc & M64);
+        fe q = rb ? num / rb : 0, r = rb ? num % rb : num;
+        imm = rc;
+        next[op->dst] = q & M64;
+        next[op->dst2] = r & M64;
+        inv = rb ? fe_inv(rb & M64) : 0;
+        break;
+      }
       default: break;
+    }
+    if (onehot >= 0 && onehot != 8 && onehot < 15) {
+      int uses_a = k_ != OP_CONST && k_ != OP_CADDR && k_ != OP_ASSERT && k_ != OP_ASSERT_BIT && k_ != OP_RANGE &&
+                   k_ != OP_RANGE_LO && k_ != OP_RANGE_HI;
+      int uses_b = k_ == OP_ADD || k_ == OP_SUB || k_ == OP_MUL || k_ == OP_EQ || k_ == OP_SELECT || k_ == OP_DIVMOD ||
+                   k_ == OP_DIV128 || k_ == OP_MULWIDE;
+      int uses_c = k_ == OP_SELECT || k_ == OP_ASSERT || k_ == OP_ASSERT_BIT || k_ == OP_RANGE || k_ == OP_RANGE_LO ||
+                   k_ == OP_RANGE_HI;
+      int uses_d1 = k_ == OP_DIVMOD || k_ == OP_DIV128 || k_ == OP_MULWIDE;
+      for (int q = 0; q < 2; q++) {
+        size_t row = rows[q];
+        set_fe(t, n, c.op[onehot], row, 1);
+        set_sel(t, n, row, c.sel_dst0, op->dst);
+        if (uses_d1) set_sel(t, n, row, c.sel_dst1, op->dst2);
+        if (uses_a) set_sel(t, n, row, c.sel_a, op->a);
+        if (uses_b) set_sel(t, n, row, c.sel_b, op->b);
+        if (uses_c) set_sel(t, n, row, c.sel_c, op->c);
+        set_fe(t, n, c.imm, row, imm);
+        set_fe(t, n, c.eq_inv, row, inv);
+        for (int i = 0; gadget && i < 32; i++) set_fe(t, n, c.gadget_b + i, row, bitv[i]);
+      }
     }
     for (size_t r = rm + 1; r <= rf; r++)
       for (int i = 0; i < NR; i++) set_fe(t, n, c.r_start + i, r, regs[i]);
@@ -401,7 +477,7 @@ int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t lo
       for (int i = 0; i < NR; i++) set_fe(t, n, c.r_start + i, r, next[i]);
     memcpy(regs, next, sizeof regs);
   }
-  if (flags & SYN_RAM) ram_fill(t, n, &c, pid, ev, n_ev);
+  if (ram) ram_fill(t, n, &c, pid, ev, n_ev);
   free(ev);
   free(mem);
   /* RomTraceBuilder (rom.rs:37-106) */
@@ -413,7 +489,7 @@ int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t lo
     a = fe_exp(3, 1037); cur = fe_mul(a, 3);
     for (int i = 0; i < 59; i++) { w1[i] = cur; cur = fe_mul(cur, 3); }
   }
-  fe s0_prev = rom0_in ? ((fe)rom0_in->hi << 64 | rom0_in->lo) : 0;
+  fe s0_prev = rom0;
   fe last_state[3] = {0, 0, 0};
   for (size_t l = 0; l < levels; l++) {
     size_t b = l * 32, rm = b, rf = b + 28;
@@ -438,19 +514,21 @@ int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t lo
     s0_prev = s[0];
     memcpy(last_state, s, sizeof s);
   }
-  free(ops);
 
   /* AIR public inputs (prove.rs:292-423 with segment = whole trace) */
   memcpy(pi->program_id, pid, 32);
-  memcpy(pi->program_commitment, pid, 32);
-  pi->feature_mask = FM_VM | ((flags & SYN_SPONGE) ? FM_SPONGE | FM_POSEIDON : 0) | ((flags & SYN_RAM) ? FM_RAM : 0) |
-                     ((flags & SYN_MERKLE) ? FM_MERKLE | FM_POSEIDON : 0);
-  if (flags & SYN_MERKLE) { /* root = acc after the MerkleStepLast level, as 16 LE bytes (utils.rs:346-355) */
-    fe root = get_fe(t, n, c.merkle_acc, 5 * 32 + 28);
+  memcpy(pi->program_commitment, commit, 32);
+  pi->feature_mask = FM_VM | (sponge ? FM_SPONGE | FM_POSEIDON : 0) | (ram ? FM_RAM : 0) |
+                     (merkle ? FM_MERKLE | FM_POSEIDON : 0);
+  long mlast = -1;
+  for (size_t l = 0; l < levels; l++) if (ops[l].kind == OP_MLAST) mlast = (long)l;
+  if (merkle && mlast >= 0) { /* root = acc after the last MerkleStepLast level, 16 LE bytes (utils.rs:346-355) */
+    fe root = get_fe(t, n, c.merkle_acc, (size_t)mlast * 32 + 28);
     for (int i = 0; i < 16; i++) pi->merkle_root[i] = (uint8_t)(root >> (8 * i));
   }
   pi->segment_feature_mask = pi->feature_mask;
-  pi->n_main_slots = 0;
+  pi->n_main_slots = n_slots;
+  for (uint32_t i = 0; i < n_slots; i++) { pi->main_slots[i].lo = (uint64_t)slots[i]; pi->main_slots[i].hi = (uint64_t)(slots[i] >> 64); }
   /* vm_output_from_trace_with_layout (utils.rs:262-289) */
   pi->vm_out_reg = 0; pi->vm_out_row = 29;
   for (size_t l = levels; l-- > 0;) {
@@ -483,7 +561,7 @@ int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t lo
     if (get_fe(t, n, c.op[8], r)) mask |= 1u << 7;
   }
   uint32_t ram_bits = 0;
-  if (flags & SYN_RAM)
+  if (ram)
     for (size_t r = 0; r + 1 < n; r++)
       if (get_fe(t, n, c.ram_sorted, r) && get_fe(t, n, c.ram_sorted, r + 1) &&
           get_fe(t, n, c.ram_s_addr, r) == get_fe(t, n, c.ram_s_addr, r + 1)) {
@@ -493,4 +571,89 @@ int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t lo
   pi->vm_usage_mask = mask;
   pi->ram_delta_clk_bits = ram_bits;
   return 0;
+}
+
+/* the synthetic program with ROM lane 0 entering the first level at *rom0_in (the accumulator
+ * lane the aggregation chains across segments, agg/trace.rs:524-541) instead of 0 */
+int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t log_n, uint32_t flags, const zkl_f128 *rom0_in, zkl_f128 *t,
+                               zkl_air_public_inputs *pi, uint32_t *width_out) {
+  if (log_n < 5 || log_n > 26 || (flags & ~7u)) return -1;
+  if ((flags & SYN_MERKLE) && log_n < 8) return -1;
+  size_t n = (size_t)1 << log_n, levels = n / 32;
+  zk_cols c;
+  cols_for_config(1, !!(flags & SYN_RAM), !!(flags & SYN_SPONGE), !!(flags & SYN_MERKLE), 1, &c);
+  if (width_out) *width_out = (uint32_t)c.width;
+  if (!t) return 0;
+  char desc[160];
+  snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 %s%s%sseed=0x%016llx levels=%zu",
+           (flags & SYN_SPONGE) ? "sponge " : "", (flags & SYN_RAM) ? "ram " : "", (flags & SYN_MERKLE) ? "merkle " : "",
+           (unsigned long long)program_seed, levels);
+  uint8_t pid[32];
+  orc_blake3((const uint8_t *)desc, strlen(desc), pid);
+  synth_op *ops = (synth_op *)malloc(levels * sizeof(synth_op));
+  synth_program(seed, levels, ops, flags);
+  fe regs0[NR] = {0};
+  int rc = build_core(ops, levels, pid, pid, !!(flags & SYN_SPONGE), !!(flags & SYN_RAM), !!(flags & SYN_MERKLE),
+                      rom0_in ? ((fe)rom0_in->hi << 64 | rom0_in->lo) : 0, regs0, NULL, 0, t, pi);
+  free(ops);
+  return rc;
+}
+
+/* The op-list trace builder (zkl_build_trace's twin): builder::Op list (builder.rs:25-158)
+ * -> build_full_trace (mod.rs:434-524) over next_pow2(n_ops) levels. */
+int orc_build_trace(const zkl_op *zops, uint32_t n_ops, const uint8_t pid[32], const uint8_t commit[32],
+                    const uint64_t *secret, uint32_t n_secret, const zkl_vm_arg *margs, uint32_t n_main,
+                    const zkl_f128 *rom0_in, zkl_f128 *t, zkl_air_public_inputs *pi, uint32_t *width_out,
+                    uint32_t *n_rows_out) {
+  static const int kinds[] = {OP_CONST, OP_MOV, OP_ADD, OP_SUB, OP_MUL, OP_NEG, OP_EQ, OP_SELECT, OP_ASSERT,
+                              OP_ASSERT_BIT, OP_RANGE, OP_RANGE_LO, OP_RANGE_HI, OP_DIVMOD, OP_DIV128, OP_MULWIDE,
+                              OP_LOAD, OP_STORE, OP_ABSORB, OP_SQUEEZE, OP_MFIRST, OP_MSTEP, OP_MLAST, OP_END};
+  if (!zops || !n_ops || n_main > ZKL_MAX_MAIN_SLOTS) return -1;
+  size_t levels = 1;
+  while (levels < n_ops) levels <<= 1;
+  synth_op *ops = (synth_op *)calloc(levels, sizeof(synth_op));
+  int sponge = 0, ram = 0, merkle = 0;
+  for (size_t l = 0; l < levels; l++) {
+    synth_op *o = &ops[l];
+    if (l >= n_ops) { o->kind = OP_PAD; continue; }
+    const zkl_op *z = &zops[l];
+    if (z->kind >= sizeof kinds / sizeof kinds[0] || z->dst > 7 || z->dst2 > 7 || z->a > 7 || z->b > 7 || z->c > 7 ||
+        z->n_regs > 10 || (z->kind == ZKL_OP_ASSERT_RANGE && (z->bits < 1 || z->bits > 64)) ||
+        (z->kind == ZKL_OP_SABSORBN && z->n_regs < 1)) {
+      free(ops);
+      return -1;
+    }
+    o->kind = kinds[z->kind];
+    o->dst = z->dst; o->dst2 = z->dst2; o->a = z->a; o->b = z->b; o->c = z->c; o->bits = z->bits; o->imm = z->imm;
+    o->nabs = z->n_regs;
+    for (int i = 0; i < z->n_regs; i++) {
+      if (z->regs[i] > 7) { free(ops); return -1; }
+      o->abs_regs[i] = z->regs[i];
+    }
+    sponge |= o->kind == OP_ABSORB || o->kind == OP_SQUEEZE;
+    ram |= o->kind == OP_LOAD || o->kind == OP_STORE;
+    merkle |= o->kind == OP_MFIRST || o->kind == OP_MSTEP || o->kind == OP_MLAST;
+  }
+  zk_cols c;
+  cols_for_config(1, ram, sponge, merkle, 1, &c);
+  if (width_out) *width_out = (uint32_t)c.width;
+  if (n_rows_out) *n_rows_out = (uint32_t)(levels * 32);
+  if (!t) { free(ops); return 0; }
+  fe slots[8];
+  uint32_t ns = 0;
+  for (uint32_t i = 0; i < n_main; i++) { /* encode_vmarg_to_elements (utils.rs:79-97) */
+    const zkl_vm_arg *a = &margs[i];
+    int need = a->tag == 2 ? 2 : 1;
+    if (a->tag > 2 || ns + need > 8) { free(ops); return -1; }
+    if (a->tag == 0) { uint64_t x; memcpy(&x, a->bytes, 8); slots[ns++] = x; }
+    else { slots[ns++] = be_from_le8(a->bytes); if (a->tag == 2) slots[ns++] = be_from_le8(a->bytes + 16); }
+  }
+  fe regs0[NR] = {0};
+  uint32_t tail = NR - ns;
+  for (uint32_t i = 0; i < n_secret && i < tail; i++) regs0[i] = secret[i];
+  for (uint32_t j = 0; j < ns; j++) regs0[tail + j] = slots[j];
+  int rc = build_core(ops, levels, pid, commit, sponge, ram, merkle, rom0_in ? ((fe)rom0_in->hi << 64 | rom0_in->lo) : 0,
+                      regs0, slots, ns, t, pi);
+  free(ops);
+  return rc;
 }

@@ -3,6 +3,8 @@
 ORACLE = test infrastructure: only tests/, __graft_entry__.smoke() and bench.py's
 cpu_baseline leg load this.  The product (libzkl_hip.so) never does.
 """
+from __future__ import annotations
+
 import ctypes as C
 import os
 import subprocess
@@ -200,6 +202,27 @@ def synth_segment_chain(program_seed: int, seed: int, log_n: int, rom0: int = 0,
                                           C.c_uint32(flags), C.byref(r0), trace, C.byref(pi), C.byref(w))
     assert rc == 0
     return trace, pi, w.value
+
+
+def build_trace(ops, program_id: bytes, program_commitment: bytes | None = None, secret_args=(), main_args=None,
+                rom0: int = 0):
+    """orc_build_trace over a ctypes array of zkl_op (the product's zkl_hip.ZklOp layout) and
+    VmArg main args (ctypes array or None).  Returns (rc, trace, AirPublicInputs, W, n_rows)."""
+    commit = bytes(program_commitment if program_commitment is not None else program_id)
+    sec = (C.c_uint64 * max(1, len(secret_args)))(*secret_args)
+    n_main = 0 if main_args is None else len(main_args)
+    ma = None if main_args is None else C.cast(main_args, C.c_void_p)
+    r0 = F128(rom0 & (2 ** 64 - 1), rom0 >> 64)
+    w, n = C.c_uint32(), C.c_uint32()
+    args = (C.cast(ops, C.c_void_p), C.c_uint32(len(ops)), bytes(program_id), commit, sec, C.c_uint32(len(secret_args)),
+            ma, C.c_uint32(n_main), C.byref(r0))
+    rc = lib().orc_build_trace(*args, None, None, C.byref(w), C.byref(n))
+    if rc != 0:
+        return rc, None, None, 0, 0
+    trace = (F128 * (w.value * n.value))()
+    pi = AirPublicInputs()
+    rc = lib().orc_build_trace(*args, trace, C.byref(pi), C.byref(w), C.byref(n))
+    return rc, trace, pi, w.value, n.value
 
 
 def default_options(width, n, queries=64, blowup=16, grind=16):

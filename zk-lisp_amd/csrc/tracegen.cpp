@@ -36,10 +36,39 @@ uint64_t splitmix(uint64_t& s) {
 }
 enum Kind {
   K_CONST = 0, K_MOV = 1, K_ADD = 2, K_SUB = 3, K_MUL = 4, K_ABSORB = 10, K_SQUEEZE = 11, K_ADDR = 12,
-  K_LOAD = 15, K_STORE = 16, K_MFIRST = 20, K_MSTEP = 21, K_MLAST = 22, K_END = 99
+  K_LOAD = 15, K_STORE = 16, K_MFIRST = 20, K_MSTEP = 21, K_MLAST = 22,
+  K_NEG = 40, K_EQ, K_SELECT, K_ASSERT, K_ASSERT_BIT, K_RANGE, K_RANGE_LO, K_RANGE_HI, K_DIVMOD, K_DIV128, K_MULWIDE,
+  K_END = 99, K_PAD = 100  // K_PAD: a level past the program's last op (build_empty_trace rows only)
 };
-// Merkle steps: dst = leaf register, a = dir register, b = sibling register
-struct Op { Kind k; int dst, a, b; uint64_t imm; int nabs; int abs_regs[3]; };
+// Merkle steps: dst = leaf register, a = dir register, b = sibling register.  dst2: the second
+// destination (DivMod r, MulWide hi, DivMod128 r); c: condition / range register (Select,
+// Assert*, AssertRange*) or a_lo (DivMod128); bits: AssertRange width.
+struct Op { Kind k; int dst, a, b; uint64_t imm; int nabs; int abs_regs[10]; int c, dst2, bits; };
+// op_to_one_hot (vm.rs:890-922): the op column / ROM one-hot index of a kind, -1 for none
+int onehot_of(Kind k) {
+  switch (k) {
+    case K_CONST: case K_ADDR: return 0;
+    case K_MOV: return 1;
+    case K_ADD: return 2;
+    case K_SUB: return 3;
+    case K_MUL: return 4;
+    case K_NEG: return 5;
+    case K_EQ: return 6;
+    case K_SELECT: return 7;
+    case K_ABSORB: case K_SQUEEZE: return 8;
+    case K_ASSERT: return 9;
+    case K_ASSERT_BIT: return 10;
+    case K_RANGE: case K_RANGE_LO: case K_RANGE_HI: return 11;
+    case K_DIVMOD: return 12;
+    case K_DIV128: return 13;
+    case K_MULWIDE: return 14;
+    case K_LOAD: return 15;
+    case K_STORE: return 16;
+    default: return -1;
+  }
+}
+unsigned __int128 as_u128(fe v) { return ((unsigned __int128)v.hi << 64) | v.lo; }
+fe from_u64(uint64_t x) { return fe{x, 0}; }
 constexpr int ADDR_REG = 7;
 
 struct RamEvent { fe addr, clk, val, w; };
@@ -126,8 +155,9 @@ std::vector<Op> make_program(uint64_t seed, size_t levels, uint32_t flags) {
   }
   if ((flags & ZKL_SYN_MERKLE) && levels >= 8) {
     uint64_t r = splitmix(st);
-    const Op m[5] = {{K_CONST, 5, 0, 0, r & 1, 0, {}}, {K_CONST, 6, 0, 0, (r >> 1) & 1, 0, {}},
-                     {K_MFIRST, 0, 5, 1, 0, 0, {}}, {K_MSTEP, 0, 6, 2, 0, 0, {}}, {K_MLAST, 0, 5, 3, 0, 0, {}}};
+    const Op m[5] = {{K_CONST, 5, 0, 0, r & 1, 0, {}, 0, 0, 0}, {K_CONST, 6, 0, 0, (r >> 1) & 1, 0, {}, 0, 0, 0},
+                     {K_MFIRST, 0, 5, 1, 0, 0, {}, 0, 0, 0}, {K_MSTEP, 0, 6, 2, 0, 0, {}, 0, 0, 0},
+                     {K_MLAST, 0, 5, 3, 0, 0, {}, 0, 0, 0}};
     for (int i = 0; i < 5; i++) ops[1 + i] = m[i];
   }
   ops[levels - 1] = Op{};
@@ -224,28 +254,22 @@ extern "C" int zkl_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t f
   return zkl_synth_vm_segment_chain(seed, seed, log_n, flags, nullptr, trace, pi, width_out);
 }
 
-extern "C" int zkl_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t log_n, uint32_t flags, const zkl_f128* rom0_in,
-                                          zkl_f128* trace, zkl_air_public_inputs* pi, uint32_t* width_out) {
-  const uint32_t all = ZKL_SYN_SPONGE | ZKL_SYN_RAM | ZKL_SYN_MERKLE;
-  if ((flags & ~all) || log_n < 5 || log_n > 26) return ZKL_E_INVALID;
-  if ((flags & ZKL_SYN_MERKLE) && log_n < 8) return ZKL_E_INVALID;  // the path needs 8 levels
-  const bool sponge = flags & ZKL_SYN_SPONGE, ram = flags & ZKL_SYN_RAM, merkle = flags & ZKL_SYN_MERKLE;
+namespace {
+// The trace of one program (ops.size() == n / 32 levels; K_PAD past the last op) in the
+// segment layout of its features: build_full_trace (vm/trace/mod.rs:434-524) with the
+// VmTraceBuilder (vm.rs:58-888), RamTraceBuilder (ram.rs:43-271), RomTraceBuilder
+// (rom.rs:29-108), plus the AIR public inputs prove_segment derives (prove.rs:292-423).
+// regs0: the initial register file (secret args, then main-arg slots in the tail registers,
+// vm.rs:64-104); rom0: ROM lane 0 entering the first level.
+int build_core(const std::vector<Op>& ops, const uint8_t pid[32], const uint8_t commit[32], bool sponge, bool ram,
+               bool merkle, fe rom0, const fe regs0[8], const std::vector<fe>& slots, size_t n, zkl_f128* trace,
+               zkl_air_public_inputs* pi) {
   const Layout L = make_layout(true, ram, sponge, merkle, true);
-  if (width_out) *width_out = (uint32_t)L.width;
-  if (!trace) return ZKL_OK;
-  if (!pi) return ZKL_E_INVALID;
-  const size_t n = (size_t)1 << log_n, levels = n / 32;
+  const size_t levels = n / 32;
   memset(trace, 0, sizeof(zkl_f128) * L.width * n);
   memset(pi, 0, sizeof *pi);
   Table T{trace, n};
-
-  char desc[160];
-  snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 %s%s%sseed=0x%016llx levels=%zu",
-           sponge ? "sponge " : "", ram ? "ram " : "", merkle ? "merkle " : "", (unsigned long long)program_seed, levels);
-  uint8_t pid[32];
-  blake3_hash((const uint8_t*)desc, strlen(desc), pid);
   PoseidonSuite ps = derive_poseidon_suite(pid, 27);
-  const std::vector<Op> ops = make_program(seed, levels, flags);
 
   // schedule gates, pc, domain tags (mod.rs:386-470)
   for (size_t l = 0; l < levels; l++) {
@@ -258,7 +282,8 @@ extern "C" int zkl_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, 
     T.set(L.lanes_start + 11, b, ps.dom[1]);
   }
   // VmTraceBuilder
-  fe regs[8] = {};
+  fe regs[8];
+  memcpy(regs, regs0, sizeof regs);
   int pending[10], npending = 0;
   std::vector<RamEvent> events;
   std::vector<std::pair<fe, fe>> mem;  // host memory: address -> last stored value
@@ -267,15 +292,23 @@ extern "C" int zkl_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, 
     fe next[8];
     memcpy(next, regs, sizeof next);
     size_t b = l * 32, rm = b, rf = b + 28;
-    if (l == 0) T.set(L.pi_prog, 0, be_from_le16(pid));
     const Op& o = ops[l];
+    if (o.k == K_PAD) continue;  // levels past the program: build_empty_trace rows only
+    if (l == 0) T.set(L.pi_prog, 0, be_from_le16(pid));
+    {
+      const int oh = onehot_of(o.k);
+      if (oh >= 0) T.set(L.rom_op_start + oh, rm, fe_one());
+    }
     switch (o.k) {
       case K_ABSORB:
       case K_SQUEEZE: {  // SAbsorbN / SSqueeze (vm.rs:565-672)
-        T.set(L.rom_op_start + 8, rm, fe_one());
         int sel_regs[10], k = 0;
         if (o.k == K_ABSORB) {
-          for (int i = 0; i < o.nabs; i++) { sel_regs[k++] = o.abs_regs[i]; pending[npending++] = o.abs_regs[i]; }
+          for (int i = 0; i < o.nabs; i++) {
+            if (npending >= 10) return ZKL_E_INVALID;  // push_absorb: sponge rate overflow (vm.rs:925-935)
+            sel_regs[k++] = o.abs_regs[i];
+            pending[npending++] = o.abs_regs[i];
+          }
         } else {
           for (int i = 0; i < npending; i++) sel_regs[k++] = pending[i];
         }
@@ -322,7 +355,6 @@ extern "C" int zkl_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, 
       case K_LOAD:
       case K_STORE: {  // Load / Store (vm.rs:803-842): clk = level; unwritten addresses read 0
         const int oh = o.k == K_LOAD ? 15 : 16;
-        T.set(L.rom_op_start + oh, rm, fe_one());
         const fe addr = regs[o.a];
         auto it = std::find_if(mem.begin(), mem.end(), [&](const std::pair<fe, fe>& e) { return fe_eq(e.first, addr); });
         for (size_t row : {rm, rf}) {
@@ -346,25 +378,97 @@ extern "C" int zkl_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, 
         break;
       }
       case K_END: break;
-      default: {  // ALU: Const / address const / Mov / Add / Sub / Mul
-        const int oh = o.k == K_ADDR ? (int)K_CONST : (int)o.k;
-        const bool is_const = o.k == K_CONST || o.k == K_ADDR;
-        T.set(L.rom_op_start + oh, rm, fe_one());
+      default: {  // ALU (vm.rs:199-564): op bit, selectors and witnesses on the map and final rows
+        const int oh = onehot_of(o.k);
+        const Kind k = o.k;
+        const bool is_const = k == K_CONST || k == K_ADDR;
+        const bool has_a = !is_const && k != K_ASSERT && k != K_ASSERT_BIT && k != K_RANGE && k != K_RANGE_LO &&
+                           k != K_RANGE_HI;
+        const bool has_b = k == K_ADD || k == K_SUB || k == K_MUL || k == K_EQ || k == K_SELECT || k == K_DIVMOD ||
+                           k == K_DIV128 || k == K_MULWIDE;
+        const bool has_c = k == K_SELECT || k == K_ASSERT || k == K_ASSERT_BIT || k == K_RANGE || k == K_RANGE_LO ||
+                           k == K_RANGE_HI;
+        const bool has_d2 = k == K_DIVMOD || k == K_DIV128 || k == K_MULWIDE;
+        fe imm = fe_zero(), eqinv = fe_zero();
+        fe bitsv[32];
+        bool gadget = false;
+        const fe va = regs[o.a], vb = regs[o.b], vc = regs[o.c];
+        const unsigned __int128 M64 = ((unsigned __int128)1 << 64) - 1;
+        switch (k) {
+          case K_CONST:
+          case K_ADDR: imm = fe{o.imm, 0}; next[o.dst] = imm; break;
+          case K_MOV: next[o.dst] = va; break;
+          case K_ADD: next[o.dst] = fe_add(va, vb); break;
+          case K_SUB: next[o.dst] = fe_sub(va, vb); break;
+          case K_MUL: next[o.dst] = fe_mul(va, vb); break;
+          case K_NEG: next[o.dst] = fe_sub(fe_zero(), va); break;
+          case K_EQ: {
+            const fe diff = fe_sub(va, vb);
+            eqinv = fe_is_zero(diff) ? fe_zero() : fe_inv(diff);
+            next[o.dst] = fe_is_zero(diff) ? fe_one() : fe_zero();
+            break;
+          }
+          case K_SELECT: next[o.dst] = fe_add(fe_mul(vc, va), fe_mul(fe_sub(fe_one(), vc), vb)); break;
+          case K_ASSERT:
+          case K_ASSERT_BIT: next[o.dst] = fe_one(); break;
+          case K_RANGE: {  // 32-bit mode: stage 1 (imm 1), mode64 0 (eq_inv 0); low min(bits, 32) bits
+            imm = fe_one();
+            unsigned __int128 x = as_u128(vc);
+            const int kb = std::min(o.bits, 32);
+            for (int i = 0; i < 32; i++) {
+              bitsv[i] = from_u64(i < kb ? (uint64_t)(x & 1) : 0);
+              if (i < kb) x >>= 1;
+            }
+            gadget = true;
+            next[o.dst] = fe_one();
+            break;
+          }
+          case K_RANGE_LO:
+          case K_RANGE_HI: {  // 64-bit stages 0 / 1: imm 0 / 1, mode64 (eq_inv 1), low / high 32 bits
+            imm = k == K_RANGE_HI ? fe_one() : fe_zero();
+            eqinv = fe_one();
+            unsigned __int128 x = as_u128(vc) >> (k == K_RANGE_HI ? 32 : 0);
+            for (int i = 0; i < 32; i++) { bitsv[i] = from_u64((uint64_t)(x & 1)); x >>= 1; }
+            gadget = true;
+            next[o.dst] = k == K_RANGE_HI ? fe_one() : from_u64((uint64_t)(as_u128(vc) & 0xFFFFFFFFu));
+            break;
+          }
+          case K_DIVMOD: {  // u128 division of the canonical values; q, r truncated to 64 bits
+            const unsigned __int128 av = as_u128(va), bv = as_u128(vb);
+            const unsigned __int128 q = bv == 0 ? 0 : av / bv, r = bv == 0 ? av : av % bv;
+            next[o.dst] = from_u64((uint64_t)(q & M64));
+            next[o.dst2] = from_u64((uint64_t)(r & M64));
+            eqinv = bv != 0 ? fe_inv(from_u64((uint64_t)bv)) : fe_zero();
+            break;
+          }
+          case K_MULWIDE: {  // (a mod 2^64)(b mod 2^64): lo -> dst0 (dst), hi -> dst1 (dst2)
+            const unsigned __int128 prod = (as_u128(va) & M64) * (as_u128(vb) & M64);
+            next[o.dst] = from_u64((uint64_t)(prod & M64));
+            next[o.dst2] = from_u64((uint64_t)(prod >> 64));
+            break;
+          }
+          case K_DIV128: {  // (a_hi 2^64 | a_lo mod 2^64) / b; a_lo rides in imm
+            imm = vc;
+            const unsigned __int128 num = (as_u128(va) << 64) | (as_u128(vc) & M64), cu = as_u128(vb);
+            const unsigned __int128 q = cu == 0 ? 0 : num / cu, r = cu == 0 ? num : num % cu;
+            next[o.dst] = from_u64((uint64_t)(q & M64));
+            next[o.dst2] = from_u64((uint64_t)(r & M64));
+            eqinv = cu != 0 ? fe_inv(from_u64((uint64_t)cu)) : fe_zero();
+            break;
+          }
+          default: return ZKL_E_INVALID;
+        }
         for (size_t row : {rm, rf}) {
           T.set(L.op[oh], row, fe_one());
           T.sel(row, L.sel_dst0, o.dst);
-          if (is_const) T.set(L.imm, row, fe{o.imm, 0});
-          else T.sel(row, L.sel_a, o.a);
-          if (o.k == K_ADD || o.k == K_SUB || o.k == K_MUL) T.sel(row, L.sel_b, o.b);
-        }
-        switch (o.k) {
-          case K_CONST:
-          case K_ADDR: next[o.dst] = fe{o.imm, 0}; break;
-          case K_MOV: next[o.dst] = regs[o.a]; break;
-          case K_ADD: next[o.dst] = fe_add(regs[o.a], regs[o.b]); break;
-          case K_SUB: next[o.dst] = fe_sub(regs[o.a], regs[o.b]); break;
-          case K_MUL: next[o.dst] = fe_mul(regs[o.a], regs[o.b]); break;
-          default: break;
+          if (has_d2) T.sel(row, L.sel_dst1, o.dst2);
+          if (has_a) T.sel(row, L.sel_a, o.a);
+          if (has_b) T.sel(row, L.sel_b, o.b);
+          if (has_c) T.sel(row, L.sel_c, o.c);
+          T.set(L.imm, row, imm);
+          T.set(L.eq_inv, row, eqinv);
+          if (gadget)
+            for (int i = 0; i < 32; i++) T.set(L.gadget_b + i, row, bitsv[i]);
         }
       }
     }
@@ -390,7 +494,7 @@ extern "C" int zkl_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, 
     for (int q = 0; q < 5; q++) for (int i = 0; i < 8; i++) s = fe_add(s, fe_mul(T.get(st[q] + i, row), w[k++]));
     return s;
   };
-  fe s0_prev = rom0_in ? fe_from(*rom0_in) : fe_zero();  // ROM lane 0 carries across segments
+  fe s0_prev = rom0;  // ROM lane 0 carries across segments
   fe last[3] = {};
   for (size_t l = 0; l < levels; l++) {
     size_t b = l * 32, rm = b, rf = b + 28;
@@ -412,12 +516,16 @@ extern "C" int zkl_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, 
   }
   // AIR public inputs for the whole-trace segment
   memcpy(pi->program_id, pid, 32);
-  memcpy(pi->program_commitment, pid, 32);
+  memcpy(pi->program_commitment, commit, 32);
   pi->feature_mask = FM_VM | (sponge ? FM_SPONGE | FM_POSEIDON : 0) | (ram ? FM_RAM : 0) |
                      (merkle ? FM_MERKLE | FM_POSEIDON : 0);
+  pi->n_main_slots = (uint32_t)slots.size();
+  for (size_t i = 0; i < slots.size(); i++) pi->main_slots[i] = to_abi(slots[i]);
   pi->segment_feature_mask = pi->feature_mask;
-  if (merkle) {  // root = acc after the MerkleStepLast level, 16 LE bytes (utils.rs:346-355)
-    const fe root = T.get(L.merkle_acc, 5 * 32 + 28);
+  long last_mlast = -1;
+  for (size_t l = 0; l < levels; l++) if (ops[l].k == K_MLAST) last_mlast = (long)l;
+  if (merkle && last_mlast >= 0) {  // root = acc after the (last) MerkleStepLast level, 16 LE bytes
+    const fe root = T.get(L.merkle_acc, (size_t)last_mlast * 32 + 28);
     for (int i = 0; i < 8; i++) {
       pi->merkle_root[i] = (uint8_t)(root.lo >> (8 * i));
       pi->merkle_root[8 + i] = (uint8_t)(root.hi >> (8 * i));
@@ -457,5 +565,181 @@ extern "C" int zkl_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, 
   }
   pi->vm_usage_mask = mask;
   pi->ram_delta_clk_bits = ram_bits;
+  return ZKL_OK;
+}
+
+// Merkle levels need the PoseidonAir-free MerkleAir block; sponge levels the PoseidonAir block;
+// Load / Store the RamAir block.  The feature set of a program is the set of blocks its ops use.
+void features_of(const std::vector<Op>& ops, bool& sponge, bool& ram, bool& merkle) {
+  sponge = ram = merkle = false;
+  for (const Op& o : ops) {
+    sponge |= o.k == K_ABSORB || o.k == K_SQUEEZE;
+    ram |= o.k == K_LOAD || o.k == K_STORE;
+    merkle |= o.k == K_MFIRST || o.k == K_MSTEP || o.k == K_MLAST;
+  }
+}
+}  // namespace
+
+extern "C" int zkl_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t log_n, uint32_t flags,
+                                          const zkl_f128* rom0_in, zkl_f128* trace, zkl_air_public_inputs* pi,
+                                          uint32_t* width_out) {
+  const uint32_t all = ZKL_SYN_SPONGE | ZKL_SYN_RAM | ZKL_SYN_MERKLE;
+  if ((flags & ~all) || log_n < 5 || log_n > 26) return ZKL_E_INVALID;
+  if ((flags & ZKL_SYN_MERKLE) && log_n < 8) return ZKL_E_INVALID;  // the path needs 8 levels
+  const bool sponge = flags & ZKL_SYN_SPONGE, ram = flags & ZKL_SYN_RAM, merkle = flags & ZKL_SYN_MERKLE;
+  const Layout L = make_layout(true, ram, sponge, merkle, true);
+  if (width_out) *width_out = (uint32_t)L.width;
+  if (!trace) return ZKL_OK;
+  if (!pi) return ZKL_E_INVALID;
+  const size_t n = (size_t)1 << log_n, levels = n / 32;
+  char desc[160];
+  snprintf(desc, sizeof desc, "zkl-hip/synthetic-vm-segment/v1 %s%s%sseed=0x%016llx levels=%zu",
+           sponge ? "sponge " : "", ram ? "ram " : "", merkle ? "merkle " : "", (unsigned long long)program_seed, levels);
+  uint8_t pid[32];
+  blake3_hash((const uint8_t*)desc, strlen(desc), pid);
+  const fe regs0[8] = {};
+  return build_core(make_program(seed, levels, flags), pid, pid, sponge, ram, merkle,
+                    rom0_in ? fe_from(*rom0_in) : fe_zero(), regs0, {}, n, trace, pi);
+}
+
+namespace {
+// zkl_op list -> Op per level, K_PAD past the last op (levels = next_pow2(n_ops), mod.rs:439)
+int to_ops(const zkl_op* ops_in, uint32_t n_ops, std::vector<Op>& ops) {
+  size_t levels = 1;
+  while (levels < n_ops) levels <<= 1;  // total_levels = levels.next_power_of_two() (mod.rs:439)
+  if (levels > ((size_t)1 << 21)) return ZKL_E_INVALID;
+  ops.assign(levels, Op{});
+  for (size_t l = 0; l < levels; l++) {
+    Op& o = ops[l];
+    o = Op{};
+    if (l >= n_ops) { o.k = K_PAD; continue; }
+    const zkl_op& z = ops_in[l];
+    if (z.dst > 7 || z.dst2 > 7 || z.a > 7 || z.b > 7 || z.c > 7 || z.n_regs > 10) return ZKL_E_INVALID;
+    o.dst = z.dst; o.dst2 = z.dst2; o.a = z.a; o.b = z.b; o.c = z.c; o.bits = z.bits; o.imm = z.imm;
+    switch (z.kind) {
+      case ZKL_OP_CONST: o.k = K_CONST; break;
+      case ZKL_OP_MOV: o.k = K_MOV; break;
+      case ZKL_OP_ADD: o.k = K_ADD; break;
+      case ZKL_OP_SUB: o.k = K_SUB; break;
+      case ZKL_OP_MUL: o.k = K_MUL; break;
+      case ZKL_OP_NEG: o.k = K_NEG; break;
+      case ZKL_OP_EQ: o.k = K_EQ; break;
+      case ZKL_OP_SELECT: o.k = K_SELECT; break;
+      case ZKL_OP_ASSERT: o.k = K_ASSERT; break;
+      case ZKL_OP_ASSERT_BIT: o.k = K_ASSERT_BIT; break;
+      case ZKL_OP_ASSERT_RANGE:
+        if (z.bits < 1 || z.bits > 64) return ZKL_E_INVALID;
+        o.k = K_RANGE;
+        break;
+      case ZKL_OP_ASSERT_RANGE_LO: o.k = K_RANGE_LO; break;
+      case ZKL_OP_ASSERT_RANGE_HI: o.k = K_RANGE_HI; break;
+      case ZKL_OP_DIVMOD: o.k = K_DIVMOD; break;
+      case ZKL_OP_DIVMOD128: o.k = K_DIV128; break;
+      case ZKL_OP_MULWIDE: o.k = K_MULWIDE; break;
+      case ZKL_OP_SABSORBN:
+        if (z.n_regs < 1) return ZKL_E_INVALID;
+        o.k = K_ABSORB;
+        o.nabs = z.n_regs;
+        for (int i = 0; i < z.n_regs; i++) {
+          if (z.regs[i] > 7) return ZKL_E_INVALID;
+          o.abs_regs[i] = z.regs[i];
+        }
+        break;
+      case ZKL_OP_SSQUEEZE: o.k = K_SQUEEZE; break;
+      case ZKL_OP_MERKLE_FIRST: o.k = K_MFIRST; break;
+      case ZKL_OP_MERKLE_STEP: o.k = K_MSTEP; break;
+      case ZKL_OP_MERKLE_LAST: o.k = K_MLAST; break;
+      case ZKL_OP_LOAD: o.k = K_LOAD; break;
+      case ZKL_OP_STORE: o.k = K_STORE; break;
+      case ZKL_OP_END: o.k = K_END; break;
+      default: return ZKL_E_INVALID;
+    }
+  }
+  return ZKL_OK;
+}
+}  // namespace
+
+extern "C" int zkl_build_trace(const zkl_op* ops_in, uint32_t n_ops, const uint8_t program_id[32],
+                               const uint8_t program_commitment[32], const uint64_t* secret_args, uint32_t n_secret,
+                               const zkl_vm_arg* main_args, uint32_t n_main, const zkl_f128* rom0_in,
+                               zkl_f128* trace, zkl_air_public_inputs* pi, uint32_t* width_out,
+                               uint32_t* n_rows_out) {
+  if (!ops_in || n_ops == 0 || !program_id || !program_commitment) return ZKL_E_INVALID;
+  if ((n_secret && !secret_args) || (n_main && !main_args) || n_main > ZKL_MAX_MAIN_SLOTS) return ZKL_E_INVALID;
+  std::vector<Op> ops;
+  if (int rc = to_ops(ops_in, n_ops, ops)) return rc;
+  const size_t levels = ops.size();
+  bool sponge, ram, merkle;
+  features_of(ops, sponge, ram, merkle);
+  const Layout L = make_layout(true, ram, sponge, merkle, true);
+  const size_t n = levels * 32;
+  if (width_out) *width_out = (uint32_t)L.width;
+  if (n_rows_out) *n_rows_out = (uint32_t)n;
+  if (!trace) return ZKL_OK;
+  if (!pi) return ZKL_E_INVALID;
+  std::vector<fe> slots;  // encode_main_args_to_slots (utils.rs:79-109)
+  for (uint32_t i = 0; i < n_main; i++) {
+    const zkl_vm_arg& a = main_args[i];
+    if (a.tag == 0) { uint64_t x; memcpy(&x, a.bytes, 8); slots.push_back(fe{x, 0}); }
+    else if (a.tag == 1) slots.push_back(be_from_le16(a.bytes));
+    else if (a.tag == 2) { slots.push_back(be_from_le16(a.bytes)); slots.push_back(be_from_le16(a.bytes + 16)); }
+    else return ZKL_E_INVALID;
+  }
+  if (slots.size() > 8) return ZKL_E_INVALID;  // "too many main_args for VM register file" (vm.rs:68-74)
+  fe regs0[8] = {};
+  const size_t tail = 8 - slots.size();  // secret args fill r0.., main-arg slots the tail (vm.rs:64-104)
+  for (size_t i = 0; i < n_secret && i < tail; i++) regs0[i] = fe{secret_args[i], 0};
+  for (size_t j = 0; j < slots.size(); j++) regs0[tail + j] = slots[j];
+  return build_core(ops, program_id, program_commitment, sponge, ram, merkle, rom0_in ? fe_from(*rom0_in) : fe_zero(),
+                    regs0, slots, n, trace, pi);
+}
+
+// rom_acc_from_program (romacc.rs:22-80): the ROM accumulator from the ops alone, over virtual
+// map rows that hold each op's opcode bit and register selectors (encode_map_row_for_op,
+// romacc.rs:82-260) — what the verifier recomputes for pi.rom_acc (prove.rs:815-821).
+extern "C" int zkl_rom_acc_from_program(const zkl_op* ops_in, uint32_t n_ops, const uint8_t program_id[32],
+                                        zkl_f128 out[3]) {
+  if (!ops_in || !n_ops || !program_id || !out) return ZKL_E_INVALID;
+  std::vector<Op> ops;
+  if (int rc = to_ops(ops_in, n_ops, ops)) return rc;
+  fe rc3[27][3], mds3[3][3], w0[59], w1[59];
+  derive_rom_constants(program_id, rc3, mds3);
+  {
+    fe c = fe_mul(fe_pow64(fe{3, 0}, 17), fe{3, 0});
+    for (int i = 0; i < 59; i++) { w0[i] = c; c = fe_mul(c, fe{3, 0}); }
+    c = fe_mul(fe_pow64(fe{3, 0}, 1037), fe{3, 0});
+    for (int i = 0; i < 59; i++) { w1[i] = c; c = fe_mul(c, fe{3, 0}); }
+  }
+  fe s[3] = {fe_zero(), fe_zero(), fe_zero()};
+  for (const Op& o : ops) {
+    // weights: 17 opcode bits, then dst0, a, b, c, dst1 selector groups of 8 (rom.rs encode order)
+    int hot[6], nh = 0;
+    const int oh = onehot_of(o.k);
+    if (oh >= 0) hot[nh++] = oh;
+    auto sel = [&](int group, int reg) { hot[nh++] = 17 + group * 8 + reg; };
+    switch (o.k) {
+      case K_CONST: case K_ADDR: case K_LOAD: sel(0, o.dst); if (o.k == K_LOAD) sel(1, o.a); break;
+      case K_MOV: case K_NEG: sel(0, o.dst); sel(1, o.a); break;
+      case K_ADD: case K_SUB: case K_MUL: case K_EQ: sel(0, o.dst); sel(1, o.a); sel(2, o.b); break;
+      case K_SELECT: sel(0, o.dst); sel(1, o.a); sel(2, o.b); sel(3, o.c); break;
+      case K_ASSERT: case K_ASSERT_BIT: case K_RANGE: case K_RANGE_LO: case K_RANGE_HI: sel(0, o.dst); sel(3, o.c); break;
+      case K_DIVMOD: case K_DIV128: case K_MULWIDE: sel(0, o.dst); sel(4, o.dst2); sel(1, o.a); sel(2, o.b); break;
+      case K_STORE: sel(1, o.a); sel(2, o.b); break;
+      default: break;  // sponge: opcode bit only; Merkle steps, End, padding: nothing
+    }
+    fe e0 = fe_zero(), e1 = fe_zero();
+    for (int i = 0; i < nh; i++) { e0 = fe_add(e0, w0[hot[i]]); e1 = fe_add(e1, w1[hot[i]]); }
+    fe st[3] = {s[0], e0, e1};
+    for (int j = 0; j < 27; j++) {
+      const fe c3[3] = {fe_cube(st[0]), fe_cube(st[1]), fe_cube(st[2])};
+      fe y[3];
+      for (int i = 0; i < 3; i++)
+        y[i] = fe_add(fe_add(fe_add(fe_mul(mds3[i][0], c3[0]), fe_mul(mds3[i][1], c3[1])), fe_mul(mds3[i][2], c3[2])),
+                      rc3[j][i]);
+      memcpy(st, y, sizeof st);
+    }
+    memcpy(s, st, sizeof s);
+  }
+  for (int i = 0; i < 3; i++) out[i] = to_abi(s[i]);
   return ZKL_OK;
 }

@@ -18,7 +18,7 @@ __all__ = [
     "FM_VM", "FM_VM_EXPECT", "FM_POSEIDON", "FM_SPONGE", "FM_MERKLE", "FM_RAM",
     "VmArg", "StepInfo", "check_request", "row_digest_rule", "verify_segment", "step_proof_encode", "step_proof_digest", "parse_step_proof", "children_root",
     "AggOptions", "agg_prove", "agg_verify", "agg_trace", "parse_agg_artifact", "synth_segment_chain", "synth_vm_segment_chain",
-    "step_info_for",
+    "step_info_for", "ZklOp", "op", "build_trace", "OP_KINDS", "rom_acc_from_program",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -155,6 +155,10 @@ def load_library():
     lib.zkl_hip_lde.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]
     lib.zkl_synth_vm_segment_chain.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, P(F128), C.c_void_p,
                                                P(AirPublicInputs), P(C.c_uint32)]
+    lib.zkl_build_trace.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                    C.c_uint32, P(F128), C.c_void_p, P(AirPublicInputs), P(C.c_uint32),
+                                    P(C.c_uint32)]
+    lib.zkl_rom_acc_from_program.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, P(F128)]
     lib.zkl_agg_prove.argtypes = [P(C.c_char_p), P(C.c_size_t), C.c_uint32, P(AggOptions), P(P(C.c_uint8)),
                                   P(C.c_size_t), C.c_void_p]
     lib.zkl_agg_verify.argtypes = [C.c_char_p, C.c_size_t, C.c_uint32]
@@ -589,3 +593,111 @@ class Context:
                                   C.c_void_p(d_lde))
         if rc:
             self._err(rc)
+
+
+class ZklOp(C.Structure):
+    """zkl_op (include/zkl_hip.h): one zk_lisp_compiler::builder::Op (builder.rs:25-158)."""
+    _fields_ = [("kind", C.c_uint32), ("dst", C.c_uint8), ("dst2", C.c_uint8), ("a", C.c_uint8), ("b", C.c_uint8),
+                ("c", C.c_uint8), ("bits", C.c_uint8), ("n_regs", C.c_uint8), ("reserved", C.c_uint8),
+                ("regs", C.c_uint8 * 10), ("imm", C.c_uint64)]
+
+
+# builder::Op variant -> (ZKL_OP_* kind, {reference field name: zkl_op member})
+OP_KINDS = {
+    "Const": (0, {"dst": "dst", "imm": "imm"}),
+    "Mov": (1, {"dst": "dst", "src": "a"}),
+    "Add": (2, {"dst": "dst", "a": "a", "b": "b"}),
+    "Sub": (3, {"dst": "dst", "a": "a", "b": "b"}),
+    "Mul": (4, {"dst": "dst", "a": "a", "b": "b"}),
+    "Neg": (5, {"dst": "dst", "a": "a"}),
+    "Eq": (6, {"dst": "dst", "a": "a", "b": "b"}),
+    "Select": (7, {"dst": "dst", "c": "c", "a": "a", "b": "b"}),
+    "Assert": (8, {"dst": "dst", "c": "c"}),
+    "AssertBit": (9, {"dst": "dst", "r": "c"}),
+    "AssertRange": (10, {"dst": "dst", "r": "c", "bits": "bits"}),
+    "AssertRangeLo": (11, {"dst": "dst", "r": "c"}),
+    "AssertRangeHi": (12, {"dst": "dst", "r": "c"}),
+    "DivMod": (13, {"dst_q": "dst", "dst_r": "dst2", "a": "a", "b": "b"}),
+    "DivMod128": (14, {"a_hi": "a", "a_lo": "c", "b": "b", "dst_q": "dst", "dst_r": "dst2"}),
+    "MulWide": (15, {"dst_hi": "dst2", "dst_lo": "dst", "a": "a", "b": "b"}),
+    "Load": (16, {"dst": "dst", "addr": "a"}),
+    "Store": (17, {"addr": "a", "src": "b"}),
+    "SAbsorbN": (18, {"regs": "regs"}),
+    "SSqueeze": (19, {"dst": "dst"}),
+    "MerkleStepFirst": (20, {"leaf_reg": "dst", "dir_reg": "a", "sib_reg": "b"}),
+    "MerkleStep": (21, {"dir_reg": "a", "sib_reg": "b"}),
+    "MerkleStepLast": (22, {"dir_reg": "a", "sib_reg": "b"}),
+    "End": (23, {}),
+}
+
+
+def op(name: str, **fields) -> ZklOp:
+    """builder::Op by variant and field names, e.g. op("DivMod", dst_q=2, dst_r=3, a=0, b=1)."""
+    if name not in OP_KINDS:
+        raise ValueError(f"unknown op {name}")
+    kind, members = OP_KINDS[name]
+    if set(fields) != set(members):
+        raise ValueError(f"{name} takes fields {sorted(members)}, got {sorted(fields)}")
+    o = ZklOp()
+    o.kind = kind
+    for k, v in fields.items():
+        m = members[k]
+        if m == "regs":
+            if not 1 <= len(v) <= 10:
+                raise ValueError("SAbsorbN takes 1..10 registers")
+            o.n_regs = len(v)
+            o.regs[:len(v)] = list(v)
+        else:
+            setattr(o, m, v)
+    return o
+
+
+def _vm_args(main_args):
+    """main_args as VmArg list: ints (< 2^64: U64, else U128) or (tag, bytes) pairs."""
+    out = (VmArg * max(1, len(main_args)))()
+    for i, a in enumerate(main_args):
+        if isinstance(a, int):
+            out[i].tag = 0 if a < 2 ** 64 else 1
+            out[i].bytes[:16] = a.to_bytes(16, "little")
+        else:
+            out[i].tag = a[0]
+            b = bytes(a[1])
+            out[i].bytes[:len(b)] = b
+    return out
+
+
+def build_trace(ops, program_id: bytes, program_commitment: bytes | None = None, secret_args=(), main_args=(),
+                rom0: int = 0):
+    """build_full_trace (vm/trace/mod.rs:434-524) of an op list through zkl_build_trace:
+    (trace, AirPublicInputs, width, n_rows), the trace column-major in the segment layout of the
+    ops' features.  program_commitment defaults to program_id (the AIR binds pi_prog at row 0 to
+    the commitment, air/mod.rs)."""
+    lib = load_library()
+    arr = (ZklOp * len(ops))(*ops)
+    commit = bytes(program_commitment if program_commitment is not None else program_id)
+    sec = (C.c_uint64 * max(1, len(secret_args)))(*secret_args)
+    ma = _vm_args(list(main_args))
+    r0 = F128(rom0 & (2 ** 64 - 1), rom0 >> 64)
+    w, n = C.c_uint32(), C.c_uint32()
+    args = (C.cast(arr, C.c_void_p), len(ops), bytes(program_id), commit, C.cast(sec, C.c_void_p), len(secret_args),
+            C.cast(ma, C.c_void_p), len(main_args), C.byref(r0))
+    rc = lib.zkl_build_trace(*args, None, None, C.byref(w), C.byref(n))
+    if rc != 0:
+        raise ZklError(rc, "build_trace: invalid program")
+    trace = (F128 * (w.value * n.value))()
+    pi = AirPublicInputs()
+    rc = lib.zkl_build_trace(*args, C.cast(trace, C.c_void_p), C.byref(pi), C.byref(w), C.byref(n))
+    if rc != 0:
+        raise ZklError(rc, "build_trace: invalid program")
+    return trace, pi, w.value, n.value
+
+
+def rom_acc_from_program(ops, program_id: bytes):
+    """romacc::rom_acc_from_program (romacc.rs:22-80) through zkl_rom_acc_from_program: 3 ints."""
+    lib = load_library()
+    arr = (ZklOp * len(ops))(*ops)
+    out = (F128 * 3)()
+    rc = lib.zkl_rom_acc_from_program(C.cast(arr, C.c_void_p), len(ops), bytes(program_id), out)
+    if rc != 0:
+        raise ZklError(rc, "rom_acc_from_program: invalid program")
+    return [e.lo | (e.hi << 64) for e in out]
