@@ -307,6 +307,23 @@ int zkl_build_trace(const zkl_op* ops, uint32_t n_ops, const uint8_t program_id[
  * lib.rs:210-214).  Equals the trace's rom_acc for a one-segment trace built from rom0 = 0. */
 int zkl_rom_acc_from_program(const zkl_op* ops, uint32_t n_ops, const uint8_t program_id[32], zkl_f128 out[3]);
 
+/* WinterfellSegmentPlanner::plan_segments (segment_planner.rs:93-276): the row ranges
+ * [r_starts[i], r_ends[i]) of the segments of an n_ops program with at most max_rows rows per
+ * segment (the reference's default is 1 << 12, ZKL_MAX_SEGMENT_ROWS).  r_starts / r_ends NULL:
+ * only *count; otherwise cap >= *count entries are written. */
+int zkl_plan_segments(uint32_t n_ops, uint32_t max_rows, uint32_t* r_starts, uint32_t* r_ends, uint32_t cap,
+                      uint32_t* count);
+/* prove_segment's inputs for rows [r_start, r_end) of a zkl_build_trace trace (prove.rs:1057-1134):
+ * the segment feature mask from the ops of its levels (segment_planner.rs:283-334), the columns of
+ * that layout (slice_trace_segment_with_layout), the AIR public inputs with the boundary values
+ * (compute_segment_boundary_bytes, prove.rs:1197-1287) and the segment-local VM output / usage
+ * mask (build_air_pi_for_trace), and the VM state hashes of its first and last rows
+ * (utils::vm_state_hash_row_with_layout, for the zl1 step).  r_start, r_end multiples of 32,
+ * r_end - r_start a power of two.  trace_out NULL: only *width_out. */
+int zkl_slice_segment(const zkl_f128* full, uint32_t full_width, uint32_t n_full, const zkl_op* ops, uint32_t n_ops,
+                      const zkl_air_public_inputs* pi_full, uint32_t r_start, uint32_t r_end, zkl_f128* trace_out,
+                      zkl_air_public_inputs* pi_out, uint32_t* width_out, uint8_t state_in[32], uint8_t state_out[32]);
+
 /* ---- zl1 step proof (host-side, no device work) ----------------------------------
  * StepProof::to_bytes (proof/step.rs:79-151) of the step proof prove_segment builds around
  * an inner proof from zkl_hip_prove_segment*: "ZKLSTP1" | lambda | suite | core pi |

@@ -72,7 +72,11 @@ static void rom_weights(uint32_t seed, fe out[59]) {  // utils.rs:95-121
   for (int i = 0; i < 59; i++) { out[i] = cur; cur = fe_mul(cur, fe{3, 0}); }
 }
 
-std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n, AirInstance& A) {
+// check_width false: the aggregation's child replay (agg/fs.rs:38-80), which rebuilds the AIR
+// with segment_feature_mask 0 as the reference does: ZkLispAir::new then takes the layout of the
+// program's mask for a narrow trace without comparing widths (vm/air/mod.rs:141-163); only the
+// constraint degrees (composition column count) are used.
+std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n, AirInstance& A, bool check_width) {
   A = AirInstance{};
   A.n = n;
   uint64_t eff = pi.segment_feature_mask ? pi.segment_feature_mask : pi.feature_mask;
@@ -83,7 +87,7 @@ std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n,
   Layout base = make_layout(true, true, true, true, true);
   Layout cols = (int)width < base.width ? make_layout(f_vm, f_ram, f_sponge, f_merkle, pid_nz)
                                         : make_layout(true, true, true, true, pid_nz);
-  if (cols.width != (int)width) return "trace width does not match the layout implied by the feature mask";
+  if (check_width && cols.width != (int)width) return "trace width does not match the layout implied by the feature mask";
   if (com_nz != pid_nz) return "program_id / program_commitment zero-ness differs (ROM block would be inconsistent)";
 
   AirDevice& d = A.dev;

@@ -61,7 +61,8 @@ struct AirInstance {
 
 // ZkLispAir::new + get_assertions (vm/air/mod.rs:114-318, 380-504).
 // Returns empty string on success, error text otherwise.
-std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n, AirInstance& out);
+std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n, AirInstance& out,
+                      bool check_width = true);
 
 // AirPublicInputs::to_elements (lib.rs:116-160)
 std::vector<fe> pi_elements(const zkl_air_public_inputs& pi);

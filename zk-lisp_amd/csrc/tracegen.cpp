@@ -255,6 +255,40 @@ extern "C" int zkl_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t f
 }
 
 namespace {
+// vm_output_from_trace_with_layout (utils.rs:262-289) and compute_vm_usage_mask_for_trace
+// (prove.rs:1289-1392) of a (segment) trace in layout L
+void derive_trace_pi(const Table& T, const Layout& L, bool ram, size_t levels, zkl_air_public_inputs* pi) {
+  const size_t n = T.n;
+  pi->vm_out_reg = 0;
+  pi->vm_out_row = 29;
+  for (size_t l = levels; l-- > 0;) {  // vm_output_from_trace_with_layout (utils.rs:262-289)
+    size_t rf = l * 32 + 28;
+    int found = -1;
+    for (int i = 0; i < 8 && found < 0; i++) if (fe_eq(T.get(L.sel_dst0 + i, rf), fe_one())) found = i;
+    if (found >= 0) { pi->vm_out_reg = (uint32_t)found; pi->vm_out_row = (uint32_t)(rf + 1); break; }
+  }
+  uint32_t mask = 0, ram_bits = 0;  // compute_vm_usage_mask_for_trace (prove.rs:1289-1392)
+  for (size_t r = 0; r < n; r++) {
+    bool fin = (r % 32) == 28;
+    auto nz = [&](int k) { return T.nz(L.op[k], r); };
+    if (fin && (nz(9) || nz(7))) mask |= 1u << 0;
+    if (fin && nz(10)) mask |= 1u << 1;
+    if (fin && nz(11)) mask |= 1u << 2;
+    if (fin && nz(12)) mask |= 1u << 3;
+    if (fin && nz(14)) mask |= 1u << 4;
+    if (fin && nz(13)) mask |= 1u << 5;
+    if (fin && nz(6)) mask |= 1u << 6;
+    if (nz(8)) mask |= 1u << 7;
+    if (ram && r + 1 < n && T.nz(L.ram_sorted, r) && T.nz(L.ram_sorted, r + 1) &&
+        fe_eq(T.get(L.ram_s_addr, r), T.get(L.ram_s_addr, r + 1))) {
+      mask |= 1u << 8;
+      for (int i = 0; i < 32; i++) if (T.nz(L.gadget_b + i, r)) ram_bits |= 1u << i;
+    }
+  }
+  pi->vm_usage_mask = mask;
+  pi->ram_delta_clk_bits = ram_bits;
+}
+
 // The trace of one program (ops.size() == n / 32 levels; K_PAD past the last op) in the
 // segment layout of its features: build_full_trace (vm/trace/mod.rs:434-524) with the
 // VmTraceBuilder (vm.rs:58-888), RamTraceBuilder (ram.rs:43-271), RomTraceBuilder
@@ -531,45 +565,18 @@ int build_core(const std::vector<Op>& ops, const uint8_t pid[32], const uint8_t 
       pi->merkle_root[8 + i] = (uint8_t)(root.hi >> (8 * i));
     }
   }
-  pi->vm_out_reg = 0;
-  pi->vm_out_row = 29;
-  for (size_t l = levels; l-- > 0;) {  // vm_output_from_trace_with_layout (utils.rs:262-289)
-    size_t rf = l * 32 + 28;
-    int found = -1;
-    for (int i = 0; i < 8 && found < 0; i++) if (fe_eq(T.get(L.sel_dst0 + i, rf), fe_one())) found = i;
-    if (found >= 0) { pi->vm_out_reg = (uint32_t)found; pi->vm_out_row = (uint32_t)(rf + 1); break; }
-  }
   for (int i = 0; i < 3; i++) {
     pi->rom_acc[i] = to_abi(last[i]);
     pi->rom_s_in[i] = to_abi(T.get(L.rom_s + i, 0));
     pi->rom_s_out[i] = to_abi(T.get(L.rom_s + i, (levels - 1) * 32 + 28));
   }
   pi->pc_init = to_abi(T.get(L.pc, 0));
-  uint32_t mask = 0, ram_bits = 0;  // compute_vm_usage_mask_for_trace (prove.rs:1289-1392)
-  for (size_t r = 0; r < n; r++) {
-    bool fin = (r % 32) == 28;
-    auto nz = [&](int k) { return T.nz(L.op[k], r); };
-    if (fin && (nz(9) || nz(7))) mask |= 1u << 0;
-    if (fin && nz(10)) mask |= 1u << 1;
-    if (fin && nz(11)) mask |= 1u << 2;
-    if (fin && nz(12)) mask |= 1u << 3;
-    if (fin && nz(14)) mask |= 1u << 4;
-    if (fin && nz(13)) mask |= 1u << 5;
-    if (fin && nz(6)) mask |= 1u << 6;
-    if (nz(8)) mask |= 1u << 7;
-    if (ram && r + 1 < n && T.nz(L.ram_sorted, r) && T.nz(L.ram_sorted, r + 1) &&
-        fe_eq(T.get(L.ram_s_addr, r), T.get(L.ram_s_addr, r + 1))) {
-      mask |= 1u << 8;
-      for (int i = 0; i < 32; i++) if (T.nz(L.gadget_b + i, r)) ram_bits |= 1u << i;
-    }
-  }
-  pi->vm_usage_mask = mask;
-  pi->ram_delta_clk_bits = ram_bits;
+  derive_trace_pi(T, L, ram, levels, pi);
   return ZKL_OK;
 }
 
-// Merkle levels need the PoseidonAir-free MerkleAir block; sponge levels the PoseidonAir block;
-// Load / Store the RamAir block.  The feature set of a program is the set of blocks its ops use.
+// SegmentFeatures::from_ops: sponge ops need the PoseidonAir block, Merkle steps the MerkleAir
+// block (with Poseidon), Load / Store the RamAir block.
 void features_of(const std::vector<Op>& ops, bool& sponge, bool& ram, bool& merkle) {
   sponge = ram = merkle = false;
   for (const Op& o : ops) {
@@ -741,5 +748,121 @@ extern "C" int zkl_rom_acc_from_program(const zkl_op* ops_in, uint32_t n_ops, co
     memcpy(s, st, sizeof s);
   }
   for (int i = 0; i < 3; i++) out[i] = to_abi(s[i]);
+  return ZKL_OK;
+}
+
+// WinterfellSegmentPlanner::plan_segments (segment_planner.rs:93-276): the level ranges tile
+// [0, next_pow2(n_ops)) contiguously, so the segments are consecutive runs of
+// max(max_rows / 32, 1) levels (one segment when the trace fits).
+extern "C" int zkl_plan_segments(uint32_t n_ops, uint32_t max_rows, uint32_t* r_starts, uint32_t* r_ends,
+                                 uint32_t cap, uint32_t* count) {
+  if (!n_ops || !count) return ZKL_E_INVALID;
+  size_t levels = 1;
+  while (levels < n_ops) levels <<= 1;
+  const size_t rows = levels * 32;
+  const size_t per = rows <= max_rows ? levels : std::max<size_t>(max_rows / 32, 1);
+  const size_t k = (levels + per - 1) / per;
+  *count = (uint32_t)k;
+  if (!r_starts || !r_ends) return ZKL_OK;
+  if (cap < k) return ZKL_E_INVALID;
+  for (size_t i = 0; i < k; i++) {
+    r_starts[i] = (uint32_t)(i * per * 32);
+    r_ends[i] = (uint32_t)(std::min(levels, (i + 1) * per) * 32);
+  }
+  return ZKL_OK;
+}
+
+namespace {
+// utils::vm_state_hash_row_with_layout (utils.rs:312-339): BLAKE3("zkl/vm/state-v1" | r0..r7 as
+// 16-byte LE integers) of one row
+void vm_state_hash(const Table& T, const Layout& L, size_t row, uint8_t out[32]) {
+  uint8_t buf[15 + 8 * 16];
+  memcpy(buf, "zkl/vm/state-v1", 15);
+  for (int i = 0; i < 8; i++) {
+    const fe v = T.get(L.r_start + i, row);
+    for (int b = 0; b < 8; b++) {
+      buf[15 + 16 * i + b] = (uint8_t)(v.lo >> (8 * b));
+      buf[15 + 16 * i + 8 + b] = (uint8_t)(v.hi >> (8 * b));
+    }
+  }
+  blake3_hash(buf, sizeof buf, out);
+}
+}  // namespace
+
+// prove_segment's trace and public inputs for rows [r_start, r_end) of a full trace
+// (prove.rs:1057-1134): the segment's own feature mask from the ops of its levels
+// (compute_segment_features_for_levels / compute_segment_feature_mask, segment_planner.rs:283-334;
+// used when it differs from the program's), the columns of that layout sliced out of the full
+// trace (slice_trace_segment_with_layout, mod.rs), the boundary values
+// (compute_segment_boundary_bytes, prove.rs:1197-1287), the segment-local VM output and usage
+// mask (build_air_pi_for_trace, prove.rs:292-423) and the VM state hashes at its first and last
+// rows (build_segment_trace_with_state_without_full).
+extern "C" int zkl_slice_segment(const zkl_f128* full, uint32_t full_width, uint32_t n_full, const zkl_op* ops_in,
+                                 uint32_t n_ops, const zkl_air_public_inputs* pi_full, uint32_t r_start,
+                                 uint32_t r_end, zkl_f128* trace_out, zkl_air_public_inputs* pi_out,
+                                 uint32_t* width_out, uint8_t state_in[32], uint8_t state_out[32]) {
+  if (!full || !ops_in || !pi_full || r_start >= r_end || r_end > n_full) return ZKL_E_INVALID;
+  if (r_start % 32 || r_end % 32) return ZKL_E_INVALID;  // segments aligned to full levels
+  const size_t m = r_end - r_start;
+  if (m & (m - 1)) return ZKL_E_INVALID;  // a Winterfell trace length
+  std::vector<Op> ops;
+  if (int rc = to_ops(ops_in, n_ops, ops)) return rc;
+  if (ops.size() * 32 != n_full) return ZKL_E_INVALID;
+  bool sp, rm, mk;
+  features_of(ops, sp, rm, mk);
+  const Layout LF = make_layout(true, rm, sp, mk, true);
+  if (LF.width != (int)full_width) return ZKL_E_INVALID;
+  // segment features over the program levels it covers (pad levels contribute none)
+  const size_t l0 = r_start / 32, l1 = std::min<size_t>(r_end / 32, n_ops);
+  std::vector<Op> seg_ops;
+  for (size_t l = l0; l < l1; l++) seg_ops.push_back(ops[l]);
+  bool ssp, srm, smk;
+  features_of(seg_ops, ssp, srm, smk);
+  const uint64_t base = pi_full->feature_mask;
+  uint64_t seg = 0;
+  if (base & FM_VM) seg |= FM_VM;
+  if (base & FM_VM_EXPECT) seg |= FM_VM_EXPECT;
+  if ((base & FM_RAM) && srm) seg |= FM_RAM;
+  if ((base & FM_MERKLE) && smk) seg |= FM_MERKLE;
+  if ((base & FM_SPONGE) && ssp) seg |= FM_SPONGE;
+  if ((base & FM_POSEIDON) && (ssp || smk)) seg |= FM_POSEIDON;
+  const uint64_t eff = (seg != 0 && seg != base) ? seg : base;
+  const bool e_ram = eff & FM_RAM, e_merkle = eff & FM_MERKLE;
+  const Layout LS = make_layout(true, e_ram, (eff & FM_SPONGE) != 0, e_merkle, true);
+  if (width_out) *width_out = (uint32_t)LS.width;
+  if (!trace_out) return ZKL_OK;
+  if (!pi_out) return ZKL_E_INVALID;
+  if ((e_ram && !rm) || (e_merkle && !mk)) return ZKL_E_INVALID;  // a block the full trace lacks
+  // segment column -> full column: identical prefix, the optional RAM / Merkle blocks, then the
+  // tail from pi_prog on
+  auto full_col = [&](int c) {
+    if (c < LS.ram_sorted) return c;
+    if (e_ram && c < LS.ram_sorted + 8) return LF.ram_sorted + (c - LS.ram_sorted);
+    if (e_merkle && c >= LS.merkle_g && c < LS.merkle_g + 7) return LF.merkle_g + (c - LS.merkle_g);
+    return LF.pi_prog + (c - LS.pi_prog);
+  };
+  for (int c = 0; c < LS.width; c++)
+    memcpy(trace_out + (size_t)c * m, full + (size_t)full_col(c) * n_full + r_start, m * sizeof(zkl_f128));
+  const Table TF{const_cast<zkl_f128*>(full), n_full};
+  const Table TS{trace_out, m};
+  *pi_out = *pi_full;  // core inputs: ids, commitment, merkle root, base mask, main slots, rom_acc
+  pi_out->segment_feature_mask = eff;
+  pi_out->pc_init = to_abi(TF.get(LF.pc, r_start));
+  if (rm) {
+    pi_out->ram_gp_unsorted_in = to_abi(TF.get(LF.ram_gp_unsorted, r_start));
+    pi_out->ram_gp_unsorted_out = to_abi(TF.get(LF.ram_gp_unsorted, r_end - 1));
+    pi_out->ram_gp_sorted_in = to_abi(TF.get(LF.ram_gp_sorted, r_start));
+    pi_out->ram_gp_sorted_out = to_abi(TF.get(LF.ram_gp_sorted, r_end - 1));
+  } else {
+    pi_out->ram_gp_unsorted_in = pi_out->ram_gp_unsorted_out = to_abi(fe_zero());
+    pi_out->ram_gp_sorted_in = pi_out->ram_gp_sorted_out = to_abi(fe_zero());
+  }
+  for (int i = 0; i < 3; i++) {
+    pi_out->rom_s_in[i] = to_abi(TF.get(LF.rom_s + i, r_start));
+    pi_out->rom_s_out[i] = to_abi(TF.get(LF.rom_s + i, r_end - 32 + 28));
+  }
+  derive_trace_pi(TS, LS, e_ram, m / 32, pi_out);
+  if (state_in) vm_state_hash(TS, LS, 0, state_in);
+  if (state_out) vm_state_hash(TS, LS, m - 1, state_out);
   return ZKL_OK;
 }

@@ -221,7 +221,7 @@ std::string verify_segment_ex(const uint8_t* proof, size_t len, const zkl_air_pu
   const size_t n = (size_t)1 << logn, N = n * opts.blowup_factor;
   AirInstance air;
   {
-    const std::string e = build_air(pi, W, n, air);
+    const std::string e = build_air(pi, W, n, air, check_ood);
     if (!e.empty()) return "AIR construction failed: " + e;
   }
   const int C = air.num_comp_cols;

@@ -18,7 +18,7 @@ __all__ = [
     "FM_VM", "FM_VM_EXPECT", "FM_POSEIDON", "FM_SPONGE", "FM_MERKLE", "FM_RAM",
     "VmArg", "StepInfo", "check_request", "row_digest_rule", "verify_segment", "step_proof_encode", "step_proof_digest", "parse_step_proof", "children_root",
     "AggOptions", "agg_prove", "agg_verify", "agg_trace", "parse_agg_artifact", "synth_segment_chain", "synth_vm_segment_chain",
-    "step_info_for", "ZklOp", "op", "build_trace", "OP_KINDS", "rom_acc_from_program",
+    "step_info_for", "ZklOp", "op", "build_trace", "OP_KINDS", "rom_acc_from_program", "plan_segments", "slice_segment",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -159,6 +159,10 @@ def load_library():
                                     C.c_uint32, P(F128), C.c_void_p, P(AirPublicInputs), P(C.c_uint32),
                                     P(C.c_uint32)]
     lib.zkl_rom_acc_from_program.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, P(F128)]
+    lib.zkl_plan_segments.argtypes = [C.c_uint32, C.c_uint32, P(C.c_uint32), P(C.c_uint32), C.c_uint32, P(C.c_uint32)]
+    lib.zkl_slice_segment.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, P(AirPublicInputs),
+                                      C.c_uint32, C.c_uint32, C.c_void_p, P(AirPublicInputs), P(C.c_uint32),
+                                      C.c_void_p, C.c_void_p]
     lib.zkl_agg_prove.argtypes = [P(C.c_char_p), P(C.c_size_t), C.c_uint32, P(AggOptions), P(P(C.c_uint8)),
                                   P(C.c_size_t), C.c_void_p]
     lib.zkl_agg_verify.argtypes = [C.c_char_p, C.c_size_t, C.c_uint32]
@@ -701,3 +705,35 @@ def rom_acc_from_program(ops, program_id: bytes):
     if rc != 0:
         raise ZklError(rc, "rom_acc_from_program: invalid program")
     return [e.lo | (e.hi << 64) for e in out]
+
+
+def plan_segments(n_ops: int, max_rows: int = 1 << 12):
+    """WinterfellSegmentPlanner::plan_segments (segment_planner.rs:93-276): [(r_start, r_end)]."""
+    lib = load_library()
+    k = C.c_uint32()
+    if lib.zkl_plan_segments(n_ops, max_rows, None, None, 0, C.byref(k)):
+        raise ZklError(-1, "plan_segments: invalid arguments")
+    a, b = (C.c_uint32 * k.value)(), (C.c_uint32 * k.value)()
+    if lib.zkl_plan_segments(n_ops, max_rows, a, b, k.value, C.byref(k)):
+        raise ZklError(-1, "plan_segments: invalid arguments")
+    return list(zip(a, b))
+
+
+def slice_segment(full, width: int, n_rows: int, ops, pi: AirPublicInputs, r_start: int, r_end: int):
+    """prove_segment's trace + AirPublicInputs for rows [r_start, r_end) of a build_trace trace
+    (zkl_slice_segment): (trace, pi, width, state_in_hash, state_out_hash)."""
+    lib = load_library()
+    arr = (ZklOp * len(ops))(*ops)
+    w = C.c_uint32()
+    args = (C.cast(full, C.c_void_p), width, n_rows, C.cast(arr, C.c_void_p), len(ops), C.byref(pi), r_start, r_end)
+    rc = lib.zkl_slice_segment(*args, None, None, C.byref(w), None, None)
+    if rc:
+        raise ZklError(rc, "slice_segment: invalid segment")
+    m = r_end - r_start
+    t = (F128 * (w.value * m))()
+    spi = AirPublicInputs()
+    sin, sout = (C.c_uint8 * 32)(), (C.c_uint8 * 32)()
+    rc = lib.zkl_slice_segment(*args, C.cast(t, C.c_void_p), C.byref(spi), C.byref(w), sin, sout)
+    if rc:
+        raise ZklError(rc, "slice_segment: invalid segment")
+    return t, spi, w.value, bytes(sin), bytes(sout)
