@@ -423,6 +423,8 @@ def _row_digest(oracle, row, np_, rate=16):
     (51, 1000, 1),     # one partition, partial last batch of 32 rows
     (204, 1056, 4),    # trace commitment shape (4 x 51 + merge_many)
     (256, 544, 16),    # 16 partitions: merge_many absorbs over two blocks
+    (180, 96, 9),      # 9 partitions: the last count whose digests stay in registers
+    (160, 64, 10),     # 10 partitions: the LDS digest buffer form
     (7, 2048, 4),      # composition shape (one 16-wide partition + merge_many)
     (33, 96, 2),
 ])

@@ -605,10 +605,12 @@ void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np
   // partitioned rows end in merge_many (rule 0: even of one digest)
   const uint32_t merge = row_digest_rule() == 0 ? (psize != ncols) : (np_eff > 1);
   if (hash_engine() == 1 && nrows >= pm_min_items() && np_eff <= (uint32_t)PM_MAX_PARTS) {
-    if (tag == 1)
-      PM_GO(hash_rows_pm_kernel<1>, nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out);
+    if (np_eff > 9)
+      PM_GO((hash_rows_pm_kernel<0, true>), nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out);
+    else if (tag == 1)
+      PM_GO((hash_rows_pm_kernel<1, false>), nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out);
     else
-      PM_GO(hash_rows_pm_kernel<0>, nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out);
+      PM_GO((hash_rows_pm_kernel<0, false>), nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out);
     return;
   }
   if (tag == 1)
@@ -1048,6 +1050,115 @@ __global__ __launch_bounds__(THREADS) void ntt_dit_lazy_kernel(fe* __restrict__ 
   }
 }
 
+// 8-stage DIT pass held in registers: 2048 elements (8 groups of 256 at consecutive L, whole
+// 128-byte lines) on 256 threads, 8 elements per thread.  Stages 0-2 run on the elements a
+// thread loads straight from HBM (t = 8j + u), stages 3-5 and 6-7 after one LDS exchange each
+// (t = a + 8u + 64c, then two quads t = a' + 64u'), and the last quads go straight back to HBM:
+// two LDS round trips and two barriers per pass instead of five, the twiddles of a phase
+// fetched before the barrier that precedes it.  Same lazy 26-bit limb arithmetic as
+// ntt_dit_lazy_kernel (limbs < 2^31 after 8 stages).  Needs S >= 8 and N >> 8 >= 8.
+constexpr int NTT8_G = 8;
+constexpr int NTT8_THREADS = 256;
+constexpr int NTT8_PITCH = 257;
+__global__ __launch_bounds__(NTT8_THREADS) void ntt_dit8_kernel(fe* __restrict__ data, size_t ncols, int logN, int logS,
+                                                                 MontTab roots, const fe* __restrict__ src, int src_logb) {
+  __shared__ uint4 bufA[NTT8_G * NTT8_PITCH];
+  __shared__ uint32_t bufB[NTT8_G * NTT8_PITCH];
+  const int tid = (int)threadIdx.x;
+  const int g = tid & (NTT8_G - 1), j = tid >> 3;
+  // block -> (column, 8 consecutive groups); consecutive blocks walk the columns at a fixed
+  // group range so that concurrently running blocks share twiddles in L2
+  const size_t col = blockIdx.x % (unsigned)ncols;
+  const size_t q = (size_t)(blockIdx.x / (unsigned)ncols) * NTT8_G + g;
+  const size_t S = (size_t)1 << logS;
+  const size_t L = q & (S - 1), Hb = q >> logS;
+  const size_t base = (col << logN) + ((Hb << logS) << 8) + L;
+  auto tw = [&](size_t h, size_t k, uint32_t wm[5]) {
+    const size_t e = ((h + k) << logS) + L;
+    const uint4 q4 = roots.l4[e];
+    wm[0] = q4.x; wm[1] = q4.y; wm[2] = q4.z; wm[3] = q4.w; wm[4] = roots.l1[e];
+  };
+  auto bfly = [&](uint32_t x0[5], uint32_t x1[5], const uint32_t wm[5]) {
+    uint32_t v[5];
+    mont_mul(x1, wm, v);
+#pragma unroll
+    for (int l = 0; l < 5; l++) {
+      x1[l] = x0[l] + NTT_Q[l] - v[l];
+      x0[l] = x0[l] + v[l];
+    }
+  };
+  auto lds_st = [&](int t, const uint32_t x[5]) {
+    bufA[g * NTT8_PITCH + t] = make_uint4(x[0], x[1], x[2], x[3]);
+    bufB[g * NTT8_PITCH + t] = x[4];
+  };
+  auto lds_ld = [&](int t, uint32_t x[5]) {
+    const uint4 a = bufA[g * NTT8_PITCH + t];
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = bufB[g * NTT8_PITCH + t];
+  };
+  uint32_t x[8][5];
+  uint32_t w[7][5];
+  // ---- phase A: t = 8j + u, local half sizes 1, 2, 4 (twiddle k = u0 mod h)
+  tw(1, 0, w[0]);
+  tw(2, 0, w[1]); tw(2, 1, w[2]);
+#pragma unroll
+  for (int k = 0; k < 4; k++) tw(4, k, w[3 + k]);
+  {
+    const size_t Nmask = ((size_t)1 << logN) - 1;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const size_t a = base + (size_t)(8 * j + u) * S;
+      const fe v = src ? src[((a >> logN) << (logN - src_logb)) + ((a & Nmask) >> src_logb)] : data[a];
+      to26(v, x[u]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 8; u += 2) bfly(x[u], x[u + 1], w[0]);
+#pragma unroll
+  for (int u = 0; u < 8; u += 4) { bfly(x[u], x[u + 2], w[1]); bfly(x[u + 1], x[u + 3], w[2]); }
+#pragma unroll
+  for (int k = 0; k < 4; k++) bfly(x[k], x[k + 4], w[3 + k]);
+#pragma unroll
+  for (int u = 0; u < 8; u++) lds_st(8 * j + u, x[u]);
+  // ---- phase B: t = a + 8u + 64c, local half sizes 8, 16, 32 (k = a + 8 (u0 mod 2^s))
+  const int a = j & 7, c = j >> 3;
+  tw(8, a, w[0]);
+  tw(16, a, w[1]); tw(16, a + 8, w[2]);
+#pragma unroll
+  for (int k = 0; k < 4; k++) tw(32, a + 8 * k, w[3 + k]);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 8; u++) lds_ld(a + 8 * u + 64 * c, x[u]);
+#pragma unroll
+  for (int u = 0; u < 8; u += 2) bfly(x[u], x[u + 1], w[0]);
+#pragma unroll
+  for (int u = 0; u < 8; u += 4) { bfly(x[u], x[u + 2], w[1]); bfly(x[u + 1], x[u + 3], w[2]); }
+#pragma unroll
+  for (int k = 0; k < 4; k++) bfly(x[k], x[k + 4], w[3 + k]);
+  // in place: the thread's phase-B locations are its own (a partition), no barrier needed
+#pragma unroll
+  for (int u = 0; u < 8; u++) lds_st(a + 8 * u + 64 * c, x[u]);
+  // ---- phase C: two quads t = a' + 64u' (a' = j, j + 32), local half sizes 64, 128
+  tw(64, j, w[0]); tw(128, j, w[1]); tw(128, j + 64, w[2]);
+  tw(64, j + 32, w[3]); tw(128, j + 32, w[4]); tw(128, j + 96, w[5]);
+  __syncthreads();
+#pragma unroll
+  for (int qd = 0; qd < 2; qd++) {
+    const int a2 = j + 32 * qd;
+#pragma unroll
+    for (int u = 0; u < 4; u++) lds_ld(a2 + 64 * u, x[4 * qd + u]);
+    uint32_t* y0 = x[4 * qd];
+    uint32_t* y1 = x[4 * qd + 1];
+    uint32_t* y2 = x[4 * qd + 2];
+    uint32_t* y3 = x[4 * qd + 3];
+    bfly(y0, y1, w[3 * qd]);
+    bfly(y2, y3, w[3 * qd]);
+    bfly(y0, y2, w[3 * qd + 1]);
+    bfly(y1, y3, w[3 * qd + 2]);
+#pragma unroll
+    for (int u = 0; u < 4; u++) data[base + (size_t)(a2 + 64 * u) * S] = ntt_canon(x[4 * qd + u]);
+  }
+}
+
 // DIT form: lazy limbs (default) or the canonical kernel (ZKL_NTT=classic, set_ntt_lazy)
 static std::atomic<int> g_ntt_lazy{-1};
 static bool ntt_lazy_enabled() {
@@ -1070,6 +1181,16 @@ static int ntt_wide_mode() {
     return e ? atoi(e) : 2;
   }();
   return m;
+}
+
+// 8-stage register pass (ntt_dit8_kernel) for the lazy DIT passes it covers; ZKL_NTT8=0 keeps
+// the LDS-staged kernels (A/B)
+static bool ntt8_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("ZKL_NTT8");
+    return !(e && !strcmp(e, "0"));
+  }();
+  return on;
 }
 
 static int ilog2s(size_t n) { int k = 0; while (((size_t)1 << k) < n) k++; return k; }
@@ -1136,7 +1257,9 @@ static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
         const size_t Gw = wide ? 2 * G : G;
         const unsigned grid = (unsigned)((groups + Gw - 1) / Gw);
         const fe* sp = cur == lo ? src : nullptr;
-        if (wide && wm == 2)
+        if (r == 8 && ntt8_enabled() && ((size_t)1 << cur) >= (size_t)NTT8_G && (N >> 8) >= (size_t)NTT8_G)
+          ntt_dit8_kernel<<<(unsigned)(groups / NTT8_G), NTT8_THREADS, 0, s>>>(d, ncols, logN, cur, roots, sp, src_logb);
+        else if (wide && wm == 2)
           ntt_dit_lazy_kernel<2 * NTT_ELEMS, 2 * NTT_THREADS><<<grid, 2 * NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots, sp, src_logb);
         else if (wide)
           ntt_dit_lazy_kernel<2 * NTT_ELEMS, NTT_THREADS><<<grid, NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots, sp, src_logb);
