@@ -134,7 +134,8 @@ struct ProofConsts {
 };
 void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab,
                             const fe* d_bm /* (n_bcols + 1) x ce */, const CeParams& p, ProofConsts* dK,
-                            bool pose_block, bool ram_merkle, fe* d_xinv /* ce scratch */, fe* d_out,
+                            bool pose_block, bool ram_merkle,
+                            fe* d_xinv /* ce entries: 1 / (x_i - g^(n-1)) */, bool xinv_ready, fe* d_out,
                             hipStream_t s);
 // boundary vectors: vec[slot*n + step] = beta_a ; wv[s] = sum beta_a*value_a over assertions at step s
 void launch_boundary_scatter(const uint32_t* d_slot, const uint32_t* d_step, const fe* d_beta, size_t n_assert,

@@ -1395,11 +1395,12 @@ static void launch_coset_inv(const fe* d_roots, int shift, size_t M, fe a1, fe a
 }
 
 void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab, const fe* d_bm,
-                            const CeParams& p, ProofConsts* dK, bool pose_block, bool ram_merkle, fe* d_xinv, fe* d_out,
-                            hipStream_t s) {
+                            const CeParams& p, ProofConsts* dK, bool pose_block, bool ram_merkle, fe* d_xinv,
+                            bool xinv_ready, fe* d_out, hipStream_t s) {
   ZKL_HIPCHECK(hipMemcpyAsync(&dK->ce, &p, sizeof p, hipMemcpyHostToDevice, s));
   int shift = ilog2s(Ntab) - ilog2s(p.ce);
-  launch_coset_inv(d_roots, shift, p.ce, p.gl, fe_zero(), 0, d_xinv, s);  // 1 / (x - g^(n-1))
+  // 1 / (x - g^(n-1)) over the CE coset depends on the shape only: the caller keeps it per context
+  if (!xinv_ready) launch_coset_inv(d_roots, shift, p.ce, p.gl, fe_zero(), 0, d_xinv, s);
   const unsigned grid = (unsigned)((p.ce + 255) / 256);
   if (pose_block && ram_merkle)
     constraint_eval_kernel<true, true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out);

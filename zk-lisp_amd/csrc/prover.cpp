@@ -92,7 +92,10 @@ struct zkl_ctx {
   // work buffers
   DBuf trace, coef, lde, parts, tree, ce, bvec, bm, clde, ctree, deep, draws, pw, oodv, asl, ast, asv, ars;
   DBuf fri_ev, fri_tree, best, gaddr, gout, flag;
-  DBuf xinv;  // batch-inverted coset denominators (constraint evaluation, DEEP)
+  DBuf xinv;    // batch-inverted coset denominators of DEEP (z-dependent)
+  DBuf cexinv;  // 1 / (x - g^(n-1)) over the CE coset: shape-only, kept while the key matches
+  size_t cexinv_key_n = 0, cexinv_key_ce = 0, cexinv_key_tab = 0;
+  const void* cexinv_key_roots = nullptr;
   DBuf kconst;  // ProofConsts of the proof in flight on this context
   DBuf fri_coin;  // device transcript of the FRI layers: seed, alpha, layer roots
   HBuf h_asrt, h_ood, h_addr, h_gv;  // pinned staging: assertions, OOD partial sums, gather plan/values
@@ -447,9 +450,15 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->ce.ensure(ce * sizeof(fe));
   {
     KScope k(C, KF_CEVAL);
-    C->xinv.ensure(std::max(ce, N) * sizeof(fe));
+    const bool ready = C->cexinv_key_n == n && C->cexinv_key_ce == ce && C->cexinv_key_tab == Ntab &&
+                       C->cexinv_key_roots == (const void*)roots && C->cexinv.bytes >= ce * sizeof(fe);
+    if (!ready) {
+      C->cexinv_key_n = 0;  // invalid until the launch below has been queued
+      C->cexinv.ensure(ce * sizeof(fe));
+    }
     launch_constraint_eval(C->lde.f(), roots, Ntab, C->pertab.f(), C->bm.f(), cp, dK, air.dev.pose_block != 0,
-                           (air.dev.ram_block | air.dev.merkle_block) != 0, C->xinv.f(), C->ce.f(), s);
+                           (air.dev.ram_block | air.dev.merkle_block) != 0, C->cexinv.f(), ready, C->ce.f(), s);
+    C->cexinv_key_n = n; C->cexinv_key_ce = ce; C->cexinv_key_tab = Ntab; C->cexinv_key_roots = roots;
   }
   check_launch("constraint evaluation");
   T.mark(3);
