@@ -1060,16 +1060,26 @@ __global__ __launch_bounds__(THREADS) void ntt_dit_lazy_kernel(fe* __restrict__ 
 constexpr int NTT8_G = 8;
 constexpr int NTT8_THREADS = 256;
 constexpr int NTT8_PITCH = 257;
-__global__ __launch_bounds__(NTT8_THREADS) void ntt_dit8_kernel(fe* __restrict__ data, size_t ncols, int logN, int logS,
-                                                                 MontTab roots, const fe* __restrict__ src, int src_logb) {
+__global__ __launch_bounds__(NTT8_THREADS) __global__ __launch_bounds__(NTT8_THREADS) void ntt_dit8_kernel(fe* __restrict__ data, size_t ncols, int logN, int logS,
+                                                                 MontTab roots, const fe* __restrict__ src, int src_logb,
+                                                                 int lfast) {
   __shared__ uint4 bufA[NTT8_G * NTT8_PITCH];
   __shared__ uint32_t bufB[NTT8_G * NTT8_PITCH];
   const int tid = (int)threadIdx.x;
   const int g = tid & (NTT8_G - 1), j = tid >> 3;
-  // block -> (column, 8 consecutive groups); consecutive blocks walk the columns at a fixed
-  // group range so that concurrently running blocks share twiddles in L2
-  const size_t col = blockIdx.x % (unsigned)ncols;
-  const size_t q = (size_t)(blockIdx.x / (unsigned)ncols) * NTT8_G + g;
+  // block -> (column, 8 consecutive groups).  lfast = 0: consecutive blocks walk the columns
+  // at a fixed group range, so concurrently running blocks share twiddles in L2; lfast = 1:
+  // consecutive blocks take consecutive group ranges of one column, so concurrently running
+  // blocks read and write neighbouring lines of each row t (DRAM page locality)
+  size_t col, q;
+  if (lfast) {
+    const unsigned gpb = (1u << (logN - 8)) / NTT8_G;
+    col = blockIdx.x / gpb;
+    q = (size_t)(blockIdx.x % gpb) * NTT8_G + g;
+  } else {
+    col = blockIdx.x % (unsigned)ncols;
+    q = (size_t)(blockIdx.x / (unsigned)ncols) * NTT8_G + g;
+  }
   const size_t S = (size_t)1 << logS;
   const size_t L = q & (S - 1), Hb = q >> logS;
   const size_t base = (col << logN) + ((Hb << logS) << 8) + L;
@@ -1193,6 +1203,16 @@ static bool ntt8_enabled() {
   return on;
 }
 
+// block order of ntt_dit8_kernel (ZKL_NTT8_MAP): 0 = columns fastest, 1 = group ranges
+// fastest, 2 = group ranges fastest for the passes over strides S >= 2048 only
+static int ntt8_lfast(int logS) {
+  static const int m = [] {
+    const char* e = getenv("ZKL_NTT8_MAP");
+    return e ? atoi(e) : 0;
+  }();
+  return m == 1 || (m == 2 && logS >= 11) ? 1 : 0;
+}
+
 static int ilog2s(size_t n) { int k = 0; while (((size_t)1 << k) < n) k++; return k; }
 
 // Stage split of one transform into LDS passes.  The pass over the largest stride S (the
@@ -1258,7 +1278,8 @@ static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
         const unsigned grid = (unsigned)((groups + Gw - 1) / Gw);
         const fe* sp = cur == lo ? src : nullptr;
         if (r == 8 && ntt8_enabled() && ((size_t)1 << cur) >= (size_t)NTT8_G && (N >> 8) >= (size_t)NTT8_G)
-          ntt_dit8_kernel<<<(unsigned)(groups / NTT8_G), NTT8_THREADS, 0, s>>>(d, ncols, logN, cur, roots, sp, src_logb);
+          ntt_dit8_kernel<<<(unsigned)(groups / NTT8_G), NTT8_THREADS, 0, s>>>(d, ncols, logN, cur, roots, sp, src_logb,
+                                                                              ntt8_lfast(cur));
         else if (wide && wm == 2)
           ntt_dit_lazy_kernel<2 * NTT_ELEMS, 2 * NTT_THREADS><<<grid, 2 * NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots, sp, src_logb);
         else if (wide)
