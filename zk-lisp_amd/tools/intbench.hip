@@ -1,7 +1,9 @@
 // Integer VALU microbenchmarks on gfx950: throughput of the instructions the f128
-// field arithmetic is built from, and of the full Poseidon permutation.  Used to set the
-// "integer VALU peak" the roofline fraction in bench.py is priced against.
+// field arithmetic is built from, and of the full Poseidon permutation (round-1 numbers:
+// profiles/r01/intbench.txt).  bench.py's VALU ceiling now comes from the per-class rates of
+// tools/madbench.hip and the row hash's own instruction mix (tools/valu_mix.py).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdio.h>
 #include <stdint.h>
 #include <chrono>
@@ -62,18 +64,24 @@ __global__ __launch_bounds__(256) void k_fmul(fe* out, fe a) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// launch f once to warm up, then time 5 launches; any HIP failure aborts the benchmark
+#define MUST(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 template <class F>
 double timeit(F f) {
   hipEvent_t a, b;
-  hipEventCreate(&a); hipEventCreate(&b);
+  MUST(hipEventCreate(&a));
+  MUST(hipEventCreate(&b));
   f();
-  hipDeviceSynchronize();
-  hipEventRecord(a);
+  MUST(hipGetLastError());
+  MUST(hipDeviceSynchronize());
+  MUST(hipEventRecord(a));
   for (int i = 0; i < 5; i++) f();
-  hipEventRecord(b);
-  hipEventSynchronize(b);
-  float ms;
-  hipEventElapsedTime(&ms, a, b);
+  MUST(hipEventRecord(b));
+  MUST(hipEventSynchronize(b));
+  float ms = 0;
+  MUST(hipEventElapsedTime(&ms, a, b));
+  MUST(hipEventDestroy(a));
+  MUST(hipEventDestroy(b));
   return ms / 5;
 }
 
@@ -91,6 +99,6 @@ int main() {
   printf("{\"op\":\"xor+add(2 ops)\",\"G_per_s\":%.1f}\n", nthr * (double)ITERS * 8 / ms / 1e6);
   ms = timeit([&] { k_fmul<<<blocks, threads>>>((fe*)d, fe{0x123456789ull, 0x987654321ull}); });
   printf("{\"op\":\"f128_mulmod\",\"G_per_s\":%.2f}\n", nthr * (double)(ITERS / 16) * 4 / ms / 1e6);
-  hipFree(d);
+  CHECK(hipFree(d));
   return 0;
 }
