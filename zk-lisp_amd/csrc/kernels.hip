@@ -1497,7 +1497,15 @@ void launch_ood(const OodArgs& A, fe* d_partial, hipStream_t s) {
 // v_mad_u64_u32 per column into 64-bit columns (211 terms of < 2^54 stay below 2^64) and a
 // single REDC.  Each thread takes DEEP_PTS points T apart (coalesced), keeps
 // DEEP_COLS x DEEP_PTS loads in flight, and shares one inversion among its points.
-constexpr int DEEP_PTS = 4, DEEP_COLS = 4;
+// points per thread: 2 keeps the kernel at 96 VGPRs (5 waves per SIMD, more loads in flight;
+// 4 points needed 180 VGPRs, 2 waves): DEEP 0.91 -> 0.85 ms (profiles/r02/ab_deep)
+#ifndef DEEP_PTS_CFG
+#define DEEP_PTS_CFG 2
+#endif
+#ifndef DEEP_COLS_CFG
+#define DEEP_COLS_CFG 4
+#endif
+constexpr int DEEP_PTS = DEEP_PTS_CFG, DEEP_COLS = DEEP_COLS_CFG;
 
 // canonical element of the REDC output limbs (normalised, value < 2^130)
 __device__ __forceinline__ fe limbs_canon(const uint32_t l[5]) {
