@@ -135,9 +135,11 @@ def aggregate(zkl_hip, steps):
     ms = (time.perf_counter() - t0) * 1e3
     out = {"children": len(steps), "ms": round(ms, 1), "artifact_bytes": len(art), "recursion_digest": dg.hex(),
            "field_extension": "quadratic (min_security_bits 128)"}
-    g = (chain_table() or {}).get("aggregation")
-    if g and g["children"] == len(steps):
-        out["golden"] = "match" if g["sha256"] == hashlib.sha256(art).hexdigest() else "MISMATCH"
+    tab = chain_table() or {}
+    for key in ("aggregation", "aggregation_64"):  # the 8-child (configs[2]) and 64-child (configs[3]) artifacts
+        g = tab.get(key)
+        if g and g["children"] == len(steps):
+            out["golden"] = "match" if g["sha256"] == hashlib.sha256(art).hexdigest() else "MISMATCH"
     return out
 
 
@@ -152,12 +154,23 @@ def cpu_model():
 
 
 def cpu_threads(requested):
+    """Threads of the CPU baseline: every core this process may run on (sched_getaffinity;
+    BASELINE.md §2: the host's cores), unless --cpu-threads says otherwise."""
     if requested:
         return requested
-    env = os.environ.get("OMP_NUM_THREADS")
-    if env and env.isdigit() and int(env) > 0:
-        return int(env)
-    return min(16, os.cpu_count() or 1)
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def cgroup_cpu_quota():
+    """CPUs' worth of time the cgroup grants (cpu.max quota / period), or None if unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_baseline(log_n, threads, gpu_proof, log_n_target):
@@ -180,6 +193,9 @@ def cpu_baseline(log_n, threads, gpu_proof, log_n_target):
                        "grind", "queries"), (round(x / 1e3, 3) for x in orc.last_times())))
     orc.set_threads(1)
     out = {"unit": "segment-proofs/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+           "cores_available": cpu_threads(0), "cgroup_cpu_quota": cgroup_cpu_quota(),
+           "mode": "one proof using every thread (row hashing, Merkle levels, LDE columns, constraint "
+                   "evaluation, DEEP and grinding split over the threads)",
            "sample_seconds": round(dt, 2), "stage_seconds": stages}
     if log_n == log_n_target:
         out["value"] = round(1.0 / dt, 6)
@@ -325,6 +341,49 @@ class Pipeline:
             c.close()
 
 
+def host_inflight(zkl_hip, device, trace, W, n, pi, opts, steps):
+    """Two contexts proving concurrently (the reference's rayon pool calls prove_segment from
+    several threads, prove.rs:1020-1048): the same K proofs per context once from the host trace
+    (zkl_hip_prove_segment, each upload overlapping the other context's compute) and once from a
+    copy resident in HBM (zkl_hip_prove_segment_device).  Returns both rates and their ratio."""
+    import threading
+    ctxs = [zkl_hip.Context(device) for _ in range(2)]
+    nbytes = W * n * 16
+    dev = []
+    try:
+        for c in ctxs:
+            d = c.alloc(nbytes)
+            c.upload(d, trace, nbytes)
+            dev.append(d)
+            c.prove_segment(trace, W, n, pi, opts)  # warm (buffers, tables, pinned ring)
+
+        def rate(host):
+            def work(k):
+                for _ in range(steps):
+                    if host:
+                        ctxs[k].prove_segment(trace, W, n, pi, opts)
+                    else:
+                        ctxs[k].prove_segment_device(dev[k], W, n, pi, opts)
+            th = [threading.Thread(target=work, args=(k,)) for k in range(2)]
+            t0 = time.perf_counter()
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            for c in ctxs:
+                c.synchronize()
+            return 2 * steps / (time.perf_counter() - t0)
+
+        r_dev, r_host = rate(False), rate(True)
+    finally:
+        for c, d in zip(ctxs, dev):
+            c.free(d)
+        for c in ctxs:
+            c.close()
+    return {"host_trace": round(r_host, 4), "resident": round(r_dev, 4), "unit": "segment-proofs/s",
+            "fraction_of_resident_rate": round(r_host / r_dev, 4)}
+
+
 def step_info(zkl_hip, pi, index, total):
     """zl1 step metadata of segment `index` of `total`; the synthetic boundary chain is
     state_out(i) = state_in(i+1) = i+1 (what the aggregation checks)."""
@@ -370,6 +429,8 @@ def main():
                     help="configs[3] shape: distinct segments sharded over the ranks (-1: 8 x N when N > 1, else 0)")
     ap.add_argument("--inflight", type=int, default=4, help="contexts in flight per rank for --segments")
     ap.add_argument("--c5-log-n", type=int, default=20, help="rows (log2) of the configs[4] single-segment line (0: skip)")
+    ap.add_argument("--host-steps", type=int, default=5,
+                    help="proofs timed through zkl_hip_prove_segment with a host-resident trace (N = 1; 0: skip)")
     ap.add_argument("--dry-run", action="store_true", help="launcher / rank plumbing only, no device work (CPU tests)")
     args = ap.parse_args()
     if args.gpus < 1:
@@ -425,7 +486,6 @@ def main():
     nbytes = W * n * 16
     d_trace = ctx.alloc(nbytes)
     ctx.upload(d_trace, trace, nbytes)
-    del trace
     log(f"[rank {rank}] device {device}: trace {W}x{n} resident in HBM; warmup {args.warmup}")
 
     proof = None
@@ -460,11 +520,30 @@ def main():
         stages = ctx.stage_times()
         ctx.set_kernel_timing(1)
     ctx.free(d_trace)
+    # the integration entry point: zkl_hip_prove_segment with the trace in pageable host memory,
+    # as the Rust binding passes its Vec; the upload is part of every proof
+    host_line = None
+    if world == 1 and args.host_steps > 0:
+        hp = ctx.prove_segment(trace, W, n, pi, opts)
+        ctx.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.host_steps):
+            hp = ctx.prove_segment(trace, W, n, pi, opts)
+        ctx.synchronize()
+        dth = time.perf_counter() - t1
+        inflight2 = host_inflight(zkl_hip, device, trace, W, n, pi, opts, args.host_steps)
+        host_line = {"entry": "zkl_hip_prove_segment (trace in pageable host memory, uploaded inside each proof)",
+                     "value": round(args.host_steps / dth, 4), "unit": "segment-proofs/s",
+                     "ms_per_proof": round(dth / args.host_steps * 1e3, 3), "steps": args.host_steps,
+                     "trace_bytes": nbytes, "upload_loop_ms_last_proof": round(ctx.host_times().get("upload", 0.0), 3),
+                     "parity": parity_of(hp, seed, log_n)["golden"], "two_contexts_in_flight": inflight2}
+    del trace
     ctx.close()
     hand, _ = handoff(zkl_hip, dist, [(rank, pi, proof)], world)
 
     # configs[3] shape: S distinct segments sharded over the ranks, pipelined per rank
     c4 = None
+    failures = []  # any golden mismatch or failed line: parity.status MISMATCH and exit code 1
     if n_seg > 0:
         mine = dist.segments_for_rank(n_seg, rank, world)
         pl = Pipeline(zkl_hip, device, log_n, mine, max(1, min(args.inflight, len(mine))))
@@ -487,8 +566,10 @@ def main():
                   "handoff": h4}
             try:
                 c4["aggregation"] = aggregate(zkl_hip, steps4)
-            except Exception as e:  # reported, never fatal for the headline number
+            except Exception as e:  # reported in the line, and the run exits non-zero
                 c4["aggregation"] = {"error": str(e)}
+            if c4["golden_mismatches"] or "error" in c4["aggregation"] or c4["aggregation"].get("golden") == "MISMATCH":
+                failures.append("c4_sharded")
 
     if rank == 0:
         value = world * args.steps / elapsed
@@ -553,6 +634,11 @@ def main():
         }
         if c4 is not None:
             out["c4_sharded"] = c4
+        if host_line is not None:
+            host_line["fraction_of_resident_rate"] = round(host_line["value"] / value, 4)
+            out["host_trace"] = host_line
+            if host_line["parity"] == "MISMATCH":
+                failures.append("host_trace")
         if world == 1 and args.c3_segments > 0:
             c3 = {}
             for k in [int(x) for x in args.c3_inflight.split(",") if x]:
@@ -577,8 +663,11 @@ def main():
                 "unit": "segment-proofs/s", "parity": c3_par}
             try:
                 out["c3_in_gpu_pipeline"]["aggregation"] = aggregate(zkl_hip, c3_steps)
-            except Exception as e:  # reported, never fatal for the headline number
+            except Exception as e:  # reported in the line, and the run exits non-zero
                 out["c3_in_gpu_pipeline"]["aggregation"] = {"error": str(e)}
+            a3 = out["c3_in_gpu_pipeline"]["aggregation"]
+            if c3_par["golden_mismatches"] or "error" in a3 or a3.get("golden") == "MISMATCH":
+                failures.append("c3_in_gpu_pipeline")
         if world == 1 and args.c5_log_n > 0:
             try:
                 ms5, pb5 = c5_single(zkl_hip, device, args.c5_log_n)
@@ -587,19 +676,26 @@ def main():
                               "blowup 16, q 64, grind 16 (each of the 8 GPUs proves its own)",
                     "ms_per_proof": round(ms5, 1), "proof_bytes": pb5,
                     "rows_per_s": round((1 << args.c5_log_n) / ms5 * 1e3)}
-            except Exception as e:  # reported, never fatal for the headline number
+            except Exception as e:  # reported in the line, and the run exits non-zero
                 out["c5_single_segment"] = {"error": str(e)}
+                failures.append("c5_single_segment")
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(args.cpu_sample_log_n or log_n, cpu_threads(args.cpu_threads),
                                                    proof, log_n)
                 if out["cpu_baseline"].get("proof_equals_gpu_proof") is False:
-                    out["parity"]["status"] = "MISMATCH"
-            except Exception as e:  # reported, never fatal for the GPU number
+                    failures.append("cpu_baseline proof != GPU proof")
+            except Exception as e:  # reported in the line, and the run exits non-zero
                 out["cpu_baseline"] = {"value": None, "error": str(e)}
+                failures.append("cpu_baseline")
+        if out["parity"]["status"] != "ok":
+            failures.append("headline parity")
+        if failures:
+            out["parity"]["status"] = "MISMATCH"
+            out["parity"]["failed_lines"] = failures
         print(json.dumps(out), file=result_out, flush=True)
     dist.shutdown()
-    return 0
+    return 1 if failures else 0
 
 
 if __name__ == "__main__":

@@ -153,7 +153,9 @@ int zkl_hip_check_request(uint32_t width, uint32_t n_rows, const zkl_air_public_
 
 /* Host-side wall times (ms) of the last proof on ctx: [0] host setup before the first
  * kernel (AIR instance, assertions, uploads), [1] host time between the first and last
- * stage marks not covered by device work, [2] the whole call.  Returns number written. */
+ * stage marks not covered by device work, [2] the whole call, [3] the host-trace upload loop
+ * of zkl_hip_prove_segment (pinned staging + DMA issue; 0 for the device entry point).
+ * Returns number written. */
 int zkl_hip_host_times(const zkl_ctx* ctx, double* out_ms, int max_n);
 
 /* Stage timings (ms) of the last proof on ctx; returns number written.  Recorded only for
@@ -353,7 +355,22 @@ typedef struct {
   uint32_t grind;
   uint32_t min_security_bits; /* >= 128: FieldExtension::Quadratic, else None (prove.rs:647-651);
                                  >= 64: conjectured-security check (prove.rs:664-681) */
+  uint32_t trace_mode;        /* ZKL_AGG_TRACE_VALID (0) or ZKL_AGG_TRACE_REFERENCE (1), below */
 } zkl_agg_options;
+
+/* Aggregation trace modes.
+ * ZKL_AGG_TRACE_VALID: next_pow2(max(children + 1, 8)) rows (one padding row always, so the
+ *   last-row assertions of agg/air.rs:276-304 can hold) and zero root-error columns (every
+ *   opening was verified against its root under the library's row-digest rule); the batch must
+ *   satisfy ZlAggAir, otherwise ZKL_E_INVALID.  This is what zkl_agg_prove writes to proof.bin.
+ * ZKL_AGG_TRACE_REFERENCE: the trace agg/trace.rs:397-398,553-690 builds, byte for byte:
+ *   next_pow2(max(children, 8)) rows and root-error columns sum_k(root_k - root) where root_k is
+ *   reproduced from the opening's row under hash_row_poseidon (agg/child.rs:1025-1045, one chunk
+ *   not merged).  No AIR check, like the reference's release prover: for a power-of-two child
+ *   count >= 8, or children whose composition rows are one chunk (n >= 2^14), the proof does
+ *   not verify, as the reference's would not. */
+#define ZKL_AGG_TRACE_VALID 0u
+#define ZKL_AGG_TRACE_REFERENCE 1u
 
 /* What `zk-lisp prove` does after the segment proofs (replaces the Rust calls
  * RecursionPublicBuilder::build_public lib.rs:404-482, RecursionBackend::prove lib.rs:295-344
@@ -376,9 +393,12 @@ int zkl_agg_prove(const uint8_t* const* steps, const size_t* step_lens, uint32_t
 int zkl_agg_verify(const uint8_t* artifact, size_t len, uint32_t min_security_bits);
 /* The aggregation trace of the same batch (build_agg_trace_from_transcripts,
  * agg/trace.rs:155-238): 31 columns x rows, column-major; rows_out receives the row count
- * (a power of two >= 8); out may be NULL to query it. */
+ * (a power of two >= 8); out may be NULL to query it.  zkl_agg_trace builds the
+ * ZKL_AGG_TRACE_VALID trace; zkl_agg_trace_mode takes the mode. */
 int zkl_agg_trace(const uint8_t* const* steps, const size_t* step_lens, uint32_t n_steps,
                   zkl_f128* out, uint32_t max_rows, uint32_t* rows_out);
+int zkl_agg_trace_mode(const uint8_t* const* steps, const size_t* step_lens, uint32_t n_steps,
+                       uint32_t trace_mode, zkl_f128* out, uint32_t max_rows, uint32_t* rows_out);
 
 #ifdef __cplusplus
 }

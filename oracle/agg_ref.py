@@ -275,7 +275,8 @@ def child_transcript(ol, s):
     assert r.u8() == 16
     r.take(16)
     q, blowup, grind, ext, fold, rem_deg = (r.u8() for _ in range(6))
-    r.take(4)
+    r.take(2)
+    n_parts, h_rate = r.u8(), r.u8()
     nq = r.u8()
     n, N = 1 << logn, (1 << logn) * blowup
     rem_max = (rem_deg + 1) * blowup
@@ -287,7 +288,7 @@ def child_transcript(ol, s):
     fri_roots = [cm.digest() for _ in range(nl)]
     rem_commit = cm.digest()
     assert r.usize() == 1
-    tq_v, _tq_p, cq_v, _cq_p, ood_ts, ood_es = (r.vec() for _ in range(6))
+    tq_v, tq_p, cq_v, cq_p, ood_ts, ood_es = (r.vec() for _ in range(6))
     C = len(cq_v.b) // (nq * 16)  # constraint frame width from the bytes (agg/child.rs:299-340)
     layers = []
     assert r.usize() == nl
@@ -322,7 +323,61 @@ def child_transcript(ol, s):
     trows = [[tq_v.fe() for _ in range(W)] for _ in range(nq)]
     crows = [[cq_v.fe() for _ in range(C)] for _ in range(nq)]
     return dict(W=W, C=C, n=n, N=N, z=z, tz=tz, tzg=tzg, hz=hz, hzg=hzg, deep=deep, alphas=alphas[:nl],
-                positions=positions, trows=trows, crows=crows, layers=layers, remainder=remainder)
+                positions=positions, trows=trows, crows=crows, layers=layers, remainder=remainder,
+                troot=troot, croot=croot, tq_p=tq_p.b, cq_p=cq_p.b, parts=(n_parts, h_rate))
+
+
+def hash_row_poseidon(ol, row, psize):
+    """agg/child.rs:1025-1045: one digest per chunk of psize, merge_many unless one chunk."""
+    if psize == 0:
+        return ol.hash_bytes(b"")
+    d = [ol.hash_elements(row[i:i + psize]) for i in range(0, len(row), psize)]
+    return d[0] if len(d) == 1 else ol.merge_many(d)
+
+
+def _partition_size(parts, rate, ncols):  # PartitionOptions::partition_size, base field [WF-recall]
+    return ncols if parts <= 1 else max(-(-ncols // parts), rate)
+
+
+def batch_root(ol, proof, n_leaves, idx, leaves):
+    """BatchMerkleProof decompression with the given leaves (into_openings / get_root,
+    winter-crypto 0.13 [WF-recall]): the root every reconstructed path ends on."""
+    r = R(proof)
+    assert r.u8() == n_leaves.bit_length() - 1
+    lists = [[r.digest() for _ in range(r.u8())] for _ in range(r.u8())]
+    have = dict(zip(idx, leaves))
+    pairs = sorted(set(i & ~1 for i in idx))
+    assert len(pairs) == len(lists)
+    level = []  # (node index, value), sorted by index
+    for k, b in enumerate(pairs):
+        v = [have[j] if j in have else lists[k].pop(0) for j in (b, b + 1)]
+        level.append(((b + n_leaves) >> 1, ol.merge(v[0], v[1])))
+    for _ in range(1, n_leaves.bit_length() - 1):
+        nxt, i = [], 0
+        while i < len(level):
+            a, va = level[i]
+            if i + 1 < len(level) and level[i + 1][0] == a ^ 1:
+                nxt.append((a >> 1, ol.merge(va, level[i + 1][1])))
+                i += 2
+                continue
+            sib = lists[i].pop(0)  # node list of this *position* in the level (get_root's nodes[i])
+            nxt.append((a >> 1, ol.merge(sib, va) if a & 1 else ol.merge(va, sib)))
+            i += 1
+        level = nxt
+    assert len(level) == 1 and level[0][0] == 1
+    return level[0][1]
+
+
+def reference_root_errors(ol, t):
+    """trace_root_err / constraint_root_err of agg/trace.rs:553-600 for one child: the sum over
+    its queries of (root of the path rebuilt from a hash_row_poseidon leaf) - committed root."""
+    out = []
+    for rows, proof, root, w in ((t["trows"], t["tq_p"], t["troot"], t["W"]), (t["crows"], t["cq_p"], t["croot"], t["C"])):
+        ps = _partition_size(*t["parts"], w)
+        leaves = [hash_row_poseidon(ol, row, ps) for row in rows]
+        rr = batch_root(ol, proof, t["N"], t["positions"], leaves)
+        out.append(len(rows) * (rr - root) % P)
+    return out
 
 
 # ---- aggregation public inputs, trace ----------------------------------------------------
@@ -455,12 +510,14 @@ NCOLS = 31
  CNT, VMERR, RUERR, RSERR, RO0, RO1, RO2) = range(NCOLS)
 
 
-def agg_trace(ol, p, steps, txs):
-    """build_agg_trace_from_transcripts (agg/trace.rs:155-693) for an honest batch: every
-    opening of every child reproduces its commitment (the root errors are zero)."""
+def agg_trace(ol, p, steps, txs, trace_mode=0):
+    """build_agg_trace_from_transcripts (agg/trace.rs:155-693).  trace_mode 0 (the library's
+    ZKL_AGG_TRACE_VALID): one padding row always and zero root errors (every opening of every
+    child reproduces its commitment); trace_mode 1 (ZKL_AGG_TRACE_REFERENCE): the reference's
+    row count and root errors from hash_row_poseidon leaves."""
     nc = len(steps)
-    rows = 8  # next_pow2(max(children, 8)) (agg/trace.rs:396-405), keeping one padding row so
-    while rows < nc + 1:  # the last-row assertions (agg/air.rs:276-304) can hold (DESIGN.md §10)
+    rows = 8  # next_pow2(max(children, 8)) (agg/trace.rs:396-405); mode 0 keeps one padding row so
+    while rows < (nc if trace_mode == 1 else nc + 1):  # the last-row assertions (agg/air.rs:276-304) can hold
         rows *= 2
     T = [[0] * rows for _ in range(NCOLS)]
     wc = Coin(ol, agg_pi_elements(p) + [0xA9])  # derive_agg_fs_weights (agg/trace.rs:95-125)
@@ -476,6 +533,8 @@ def agg_trace(ol, p, steps, txs):
         if i + 1 == nc:
             errs = [(errs[k] + outs[k] - fin[k]) % P for k in range(4)]
         T[SEG][i], T[VCH][i], T[VACC][i], T[CNT][i] = 1, s["v_units"], v_acc, cnt
+        if trace_mode == 1:
+            T[TRE][i], T[CRE][i] = reference_root_errors(ol, t)
         T[VMERR][i], T[RUERR][i], T[RSERR][i], T[RO0][i] = errs
         fpos = _layer_positions(t)
         x0, x1 = _xs(ol, fpos[0][0], t["N"])
@@ -585,15 +644,15 @@ def _multiproof(w, tree, n_leaves, idx):
             w.digest(tree[node])
 
 
-def prove_agg(ol, T, p, queries, blowup, grind, ext):
+def prove_agg(ol, T, p, queries, blowup, grind, ext, check_air=True):
     """winterfell 0.13.1 Prover::prove for ZlAggAir [WF-recall] (prove.rs:629-719)."""
     F = Field(ext)
     Wd, n = len(T), len(T[0])
-    for i in range(n - 1):  # the trace satisfies the AIR (winterfell's debug validation)
+    for i in range(n - 1 if check_air else 0):  # the trace satisfies the AIR (winterfell's debug validation)
         tc = agg_transition([T[c][i] for c in range(Wd)], [T[c][i + 1] for c in range(Wd)], 0)
         assert not any(tc), f"aggregation trace does not satisfy ZlAggAir (row {i})"
-    assert T[OK][0] == 0 and T[VACC][0] == 0 and T[CNT][0] == 0, "aggregation trace assertion fails"
-    assert T[VACC][n - 1] == p["v_units_total"] and T[CNT][n - 1] == p["children_count"], \
+    assert not check_air or (T[OK][0] == 0 and T[VACC][0] == 0 and T[CNT][0] == 0), "aggregation trace assertion fails"
+    assert not check_air or (T[VACC][n - 1] == p["v_units_total"] and T[CNT][n - 1] == p["children_count"]), \
         "aggregation trace assertion fails"
     logn = n.bit_length() - 1
     N = n * blowup
@@ -784,13 +843,13 @@ def encode_artifact(p, proof):  # lib.rs:486-551
     return bytes(w.b)
 
 
-def agg_prove(ol, step_bytes, queries=64, blowup=16, grind=16, min_security_bits=128):
-    """steps -> (ZKLRC1 artifact, recursion digest), as zkl_agg_prove."""
+def agg_prove(ol, step_bytes, queries=64, blowup=16, grind=16, min_security_bits=128, trace_mode=0):
+    """steps -> (ZKLRC1 artifact, recursion digest, trace), as zkl_agg_prove."""
     steps = [decode_step(ol, b) for b in step_bytes]
     txs = [child_transcript(ol, s) for s in steps]
     p = build_public(ol, steps)
-    T = agg_trace(ol, p, steps, txs)
+    T = agg_trace(ol, p, steps, txs, trace_mode)
     q = max(queries, 16)
     ext = 2 if min_security_bits >= 128 else 1
-    proof = prove_agg(ol, T, p, q, blowup, grind, ext)
+    proof = prove_agg(ol, T, p, q, blowup, grind, ext, check_air=trace_mode == 0)
     return encode_artifact(p, proof), recursion_digest(ol, p), T

@@ -8,14 +8,23 @@ VM state hashes are state_in(i) = i, state_out(i) = i + 1 (32-byte LE).  The fil
 
   * rom0_in[i]: the ROM lane-0 value segment i starts from (64 entries), so each rank of a
     multi-GPU run builds only its own segments;
-  * for the first 8 segments: length and sha256 of the oracle proof at the headline options
-    (blowup 16, q 64, grind 16, partitions (4, 16));
-  * the aggregation of those 8 segments: length and sha256 of the ZKLRC1 artifact and the
-    recursion digest, from oracle/agg_ref.py over oracle-made step proofs (min_security_bits
-    128: FieldExtension::Quadratic; q 64, blowup 16, grind 16).
+  * for every one of the 64 segments: length and sha256 of the oracle proof at the headline
+    options (blowup 16, q 64, grind 16, partitions (4, 16)) -- BASELINE configs[3];
+  * "aggregation": the aggregation of the first 8 segments (steps with segments_total 8, the
+    configs[2] set): length and sha256 of the ZKLRC1 artifact and the recursion digest, from
+    oracle/agg_ref.py over oracle-made step proofs (min_security_bits 128:
+    FieldExtension::Quadratic; q 64, blowup 16, grind 16);
+  * "aggregation_64": the same over all 64 segments (steps with segments_total 64), the
+    configs[3] artifact (prove.rs:1018-1050, then lib.rs:295-551);
+  * "aggregation_ref_trace": agg_ref in the reference-trace mode (agg/trace.rs:397-398 row
+    count, hash_row_poseidon root errors) over the 16 first segments, whose
+    trace has 16 rows like the published run's (its agg proof was 52,558 B).
 
-Run (build container, ~2-3 min per proof on 8 threads):
-    python tests/golden/make_chain_goldens.py [--threads 8]
+Proof bytes are cached per segment under .chain_cache/ (git- and gpurun-ignored) so the run can
+be resumed; each proof is checked by the oracle verifier before it is used.
+
+Run (build container, ~2-3 min per proof on 8 threads; ~2.5 h for all 64):
+    python tests/golden/make_chain_goldens.py [--threads 8] [--segments 64]
 """
 import argparse
 import ctypes as C
@@ -35,46 +44,82 @@ import oracle_lib  # noqa: E402
 import zkl_hip  # noqa: E402  (only its ctypes StepInfo layout)
 
 OUT = os.path.join(HERE, "chain_2p16.json")
+CACHE = os.environ.get("ZKL_CHAIN_CACHE", os.path.join(ROOT, ".chain_cache"))
 PROGRAM = 0x5EEDC400
 LOG_N = 16
 SEGMENTS = 64
-PINNED = 8
+PINNED8 = 8
+REF_TRACE_CHILDREN = 16
+
+
+def steps_for(pis, proofs, total):
+    out = []
+    for i in range(total):
+        pi = pis[i]
+        zpi = zkl_hip.AirPublicInputs()
+        C.memmove(C.byref(zpi), C.byref(pi), C.sizeof(zpi))
+        info = zkl_hip.step_info_for(zpi, i, total, i.to_bytes(32, "little"), (i + 1).to_bytes(32, "little"))
+        out.append(oracle_lib.step_encode(pi, info, proofs[i]))
+    return out
+
+
+def agg_entry(steps, mode=0):
+    t0 = time.time()
+    art, dg, _ = agg_ref.agg_prove(oracle_lib, steps, trace_mode=mode)
+    print(f"aggregation of {len(steps)} (mode {mode}): {len(art)} bytes ({time.time() - t0:.0f}s)", flush=True)
+    return {"children": len(steps), "queries": 64, "blowup": 16, "grind": 16, "min_security_bits": 128,
+            "len": len(art), "sha256": hashlib.sha256(art).hexdigest(), "recursion_digest": dg.hex()}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("--segments", type=int, default=SEGMENTS)
+    ap.add_argument("--skip-agg", action="store_true")
+    ap.add_argument("--start", type=int, default=0, help="with --skip-agg: first segment to prove")
+    ap.add_argument("--stop", type=int, default=SEGMENTS, help="with --skip-agg: one past the last segment")
     args = ap.parse_args()
     oracle_lib.set_threads(args.threads)
+    os.makedirs(CACHE, exist_ok=True)
     n = 1 << LOG_N
-    rom0, chain = 0, []
-    pis = []
+    rom0, chain, pis = 0, [], []
     for i in range(SEGMENTS):
         chain.append(rom0)
         t, pi, w = oracle_lib.synth_segment_chain(PROGRAM, PROGRAM + i, LOG_N, rom0)
-        if i < PINNED:
-            pis.append((t, pi, w))
+        pis.append(pi)
         rom0 = pi.rom_s_out[0].lo | (pi.rom_s_out[0].hi << 64)
+        del t
     out = {"program_seed": PROGRAM, "log_n": LOG_N, "rom0_in": [hex(x) for x in chain], "segments": []}
-    steps = []
-    for i, (t, pi, w) in enumerate(pis):
-        opts = oracle_lib.default_options(w, n)
+    proofs = []
+    for i in range(args.segments):
+        if args.skip_agg and not args.start <= i < args.stop:
+            continue
+        path = os.path.join(CACHE, f"seg{i:02d}.bin")
         t0 = time.time()
-        proof = oracle_lib.prove(t, w, n, pi, opts)
-        rc, err = oracle_lib.verify(proof, pi, opts)
-        assert rc == 0, err
-        out["segments"].append({"index": i, "seed": PROGRAM + i, "width": w, "len": len(proof),
+        if os.path.exists(path):
+            proof = open(path, "rb").read()
+        else:
+            r0 = int(chain[i], 16) if isinstance(chain[i], str) else chain[i]
+            t, pi, w = oracle_lib.synth_segment_chain(PROGRAM, PROGRAM + i, LOG_N, r0)
+            opts = oracle_lib.default_options(w, n)
+            proof = oracle_lib.prove(t, w, n, pi, opts)
+            del t
+            rc, err = oracle_lib.verify(proof, pi, opts)
+            assert rc == 0, err
+            open(path + ".tmp", "wb").write(proof)
+            os.replace(path + ".tmp", path)
+        proofs.append(proof)
+        out["segments"].append({"index": i, "seed": PROGRAM + i, "width": 204, "len": len(proof),
                                 "sha256": hashlib.sha256(proof).hexdigest()})
-        zpi = zkl_hip.AirPublicInputs()
-        C.memmove(C.byref(zpi), C.byref(pi), C.sizeof(zpi))
-        info = zkl_hip.step_info_for(zpi, i, PINNED, i.to_bytes(32, "little"), (i + 1).to_bytes(32, "little"))
-        steps.append(oracle_lib.step_encode(pi, info, proof))
         print(f"segment {i}: {len(proof)} bytes ({time.time() - t0:.0f}s)", flush=True)
-    art, dg, _ = agg_ref.agg_prove(oracle_lib, steps)
-    out["aggregation"] = {"children": PINNED, "queries": 64, "blowup": 16, "grind": 16, "min_security_bits": 128,
-                          "len": len(art), "sha256": hashlib.sha256(art).hexdigest(), "recursion_digest": dg.hex()}
+    if args.skip_agg:  # proofs cached only; the golden file is left as it is
+        return
+    out["aggregation"] = agg_entry(steps_for(pis, proofs, PINNED8))
+    if args.segments >= REF_TRACE_CHILDREN:
+        out["aggregation_ref_trace"] = agg_entry(steps_for(pis, proofs, REF_TRACE_CHILDREN), mode=1)
+    if args.segments >= SEGMENTS:
+        out["aggregation_64"] = agg_entry(steps_for(pis, proofs, SEGMENTS))
     json.dump(out, open(OUT, "w"), indent=1, sort_keys=True)
-    print(json.dumps(out["aggregation"]))
 
 
 if __name__ == "__main__":

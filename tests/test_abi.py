@@ -104,7 +104,11 @@ def test_check_request_accepts_valid():
     (dict(num_partitions=17), "num_partitions"),
     (dict(num_partitions=64), "num_partitions"),
     (dict(hash_rate=0), "hash_rate"),
+    (dict(hash_rate=256), "hash_rate"),
     (dict(hash_rate=257), "hash_rate"),
+    (dict(grinding_factor=33), "grinding_factor"),
+    (dict(grinding_factor=65), "grinding_factor"),
+    (dict(blowup_factor=256), "at most 128"),
     (dict(n_main_slots=9), "ZKL_MAX_MAIN_SLOTS"),
     (dict(n_main_slots=1000), "ZKL_MAX_MAIN_SLOTS"),
     (dict(width_delta=1), "width"),

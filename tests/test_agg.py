@@ -21,14 +21,20 @@ import pyref  # noqa: E402
 PROGRAM = 0x5EEDA900
 
 
-def _steps(oracle, zkl_hip, count, log_n=5, flags=0, program=PROGRAM, break_chain_at=None, queries=8, grind=4):
-    """count chained segments -> oracle proofs -> zl1 steps (the library's encoder; test_step pins it)."""
+def _steps(oracle, zkl_hip, count, log_n=5, flags=0, program=PROGRAM, break_chain_at=None, queries=8, grind=4,
+           partitions=None):
+    """count chained segments -> oracle proofs -> zl1 steps (the library's encoder; test_step pins it).
+    partitions: force ProofOptions' num_partitions (with >= 2 the composition rows are one chunk
+    narrower than the partition, where the row-digest rules of DESIGN.md §3.1 differ)."""
     n = 1 << log_n
     rom0, out = 0, []
     for i in range(count):
         t, pi, w = oracle.synth_segment_chain(program, program + i, log_n, rom0 if i != break_chain_at else rom0 + 1,
                                               flags)
-        proof = oracle.prove(t, w, n, pi, oracle.default_options(w, n, queries=queries, grind=grind))
+        opts = oracle.default_options(w, n, queries=queries, grind=grind)
+        if partitions:
+            opts.num_partitions = partitions
+        proof = oracle.prove(t, w, n, pi, opts)
         zpi = zkl_hip.AirPublicInputs()
         C.memmove(C.byref(zpi), C.byref(pi), C.sizeof(zpi))
         info = zkl_hip.step_info_for(zpi, i, count, i.to_bytes(32, "little"), (i + 1).to_bytes(32, "little"))
@@ -98,6 +104,41 @@ def test_power_of_two_children_keep_a_padding_row(oracle, z):
     want_art, want_dg, _ = agg_ref.agg_prove(oracle, steps, grind=8)
     assert art == want_art and dg == want_dg
     z.agg_verify(art)
+
+
+@pytest.mark.parametrize("count", [3, 8])
+def test_reference_trace_mode_matches_restatement(oracle, z, count):
+    """ZKL_AGG_TRACE_REFERENCE: the trace agg/trace.rs:397-398,553-690 builds -- next_pow2(max(
+    children, 8)) rows, root errors from hash_row_poseidon leaves (agg/child.rs:1025-1045) --
+    equals agg_ref's reference mode cell for cell, and so does the artifact.  Children proved
+    with 2 partitions: their composition rows (C < 16 columns) are one chunk, which the
+    reference hashes without the merge, so every path it rebuilds ends on another root and the
+    constraint root error is num_queries x (that root - the committed root); the trace rows
+    (two chunks) give zero."""
+    steps = _steps(oracle, z, count, program=PROGRAM + 0x600 + count, queries=4, grind=0, partitions=2)
+    T1 = z.agg_trace(steps, z.AGG_TRACE_REFERENCE)
+    art, dg = z.agg_prove(steps, grind=8, trace_mode=z.AGG_TRACE_REFERENCE)
+    want_art, want_dg, want_T = agg_ref.agg_prove(oracle, steps, grind=8, trace_mode=1)
+    assert T1 == want_T
+    assert art == want_art and dg == want_dg
+    assert len(T1[0]) == 8  # no padding row for 8 children
+    T0 = z.agg_trace(steps)
+    assert len(T0[0]) == (16 if count == 8 else 8)
+    assert set(T1[agg_ref.TRE]) == {0} and set(T0[agg_ref.CRE]) == {0}
+    assert all(T1[agg_ref.CRE][i] != 0 for i in range(count)) and set(T1[agg_ref.CRE][count:]) <= {0}
+    # the reference's release prover proves this trace; it does not verify (C3 != 0, and with 8
+    # children also v_units_acc[last]); the valid mode's artifact does
+    with pytest.raises(z.ZklError):
+        z.agg_verify(art)
+    z.agg_verify(z.agg_prove(steps, grind=8)[0])
+
+
+def test_reference_trace_mode_single_chunk_rows_agree(oracle, z, chain3):
+    """With one partition (rows below 2^14) the two row-digest rules coincide: the reference
+    mode's root errors are zero and, below 8 children, its trace is the valid mode's."""
+    assert z.agg_trace(chain3, z.AGG_TRACE_REFERENCE) == z.agg_trace(chain3)
+    art1, _ = z.agg_prove(chain3, grind=8, trace_mode=z.AGG_TRACE_REFERENCE)
+    assert art1 == z.agg_prove(chain3, grind=8)[0]
 
 
 def test_aggregation_trace_layout(oracle, z, chain3):
@@ -170,6 +211,11 @@ def test_aggregation_rejections(oracle, z, chain3):
     # options below the requested 128-bit conjectured security (prove.rs:664-681)
     with pytest.raises(z.ZklError, match="min_security_bits"):
         z.agg_prove(chain3, queries=16, blowup=8, grind=0)
+    # winterfell's ProofOptions::new bound: grinding factor <= 32 (a grind > 64 could never be met)
+    with pytest.raises(z.ZklError, match="grinding factor"):
+        z.agg_prove(chain3, grind=33)
+    with pytest.raises(z.ZklError, match="trace mode"):
+        z.agg_prove(chain3, grind=8, trace_mode=2)
 
 
 def test_artifact_hash_is_stable(oracle, z, chain3):

@@ -672,56 +672,118 @@ def _chain():
     return json.load(open(p)) if os.path.exists(p) else None
 
 
-@pytest.mark.skipif(_chain() is None, reason="tests/golden/chain_2p16.json not generated")
-def test_chain_program_and_aggregation_match_goldens(oracle, gpu_ctx):
-    """BASELINE configs[2]/[3] shape end to end: the first 8 segments of the synthetic
-    multi-segment program (tests/golden/make_chain_goldens.py), proved on the GPU with 4
-    contexts in flight, equal the oracle goldens; their zl1 steps aggregate (zkl_agg_prove,
-    FieldExtension::Quadratic) into the golden ZKLRC1 artifact and recursion digest, and into
-    the artifact oracle/agg_ref.py builds from the GPU steps."""
-    import sys
+def _prove_chain(K, inflight=4):
+    """The first K segments of the synthetic chained program, proved on the GPU by `inflight`
+    contexts (one host thread each, the reference's bounded segment pool prove.rs:1018-1050),
+    wrapped as zl1 steps of a K-segment program.  Returns (proofs, steps)."""
     import threading
     import zkl_hip
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
-    import agg_ref
     ch = _chain()
     n = 1 << ch["log_n"]
-    K = len(ch["segments"])
-    segs = [zkl_hip.synth_vm_segment_chain(ch["program_seed"], ch["program_seed"] + i, ch["log_n"],
-                                           int(ch["rom0_in"][i], 16)) for i in range(K)]
-    ctxs = [zkl_hip.Context(0) for _ in range(4)]
-    dev, got = [], [None] * K
-    for k, (t, pi, w) in enumerate(segs):
-        d = ctxs[k % 4].alloc(w * n * 16)
-        ctxs[k % 4].upload(d, t, w * n * 16)
-        dev.append(d)
-
-    def run(k):
-        for i in range(k, K, 4):
-            t, pi, w = segs[i]
-            got[i] = ctxs[k].prove_segment_device(dev[i], w, n, pi, zkl_hip.proof_options(w, n))
-
+    ctxs = [zkl_hip.Context(0) for _ in range(inflight)]
+    dev, pis, got = [], [], [None] * K
     try:
-        th = [threading.Thread(target=run, args=(k,)) for k in range(4)]
+        for k in range(K):  # one host trace at a time: 64 x 214 MB stays in HBM only
+            t, pi, w = zkl_hip.synth_vm_segment_chain(ch["program_seed"], ch["program_seed"] + k, ch["log_n"],
+                                                      int(ch["rom0_in"][k], 16))
+            d = ctxs[k % inflight].alloc(w * n * 16)
+            ctxs[k % inflight].upload(d, t, w * n * 16)
+            dev.append((d, w))
+            pis.append(pi)
+            del t
+
+        def run(k):
+            for i in range(k, K, inflight):
+                d, w = dev[i]
+                got[i] = ctxs[k].prove_segment_device(d, w, n, pis[i], zkl_hip.proof_options(w, n))
+
+        th = [threading.Thread(target=run, args=(k,)) for k in range(inflight)]
         for x in th:
             x.start()
         for x in th:
             x.join()
     finally:
-        for k, d in enumerate(dev):
-            ctxs[k % 4].free(d)
+        for k, (d, _) in enumerate(dev):
+            ctxs[k % inflight].free(d)
         for c in ctxs:
             c.close()
-    for i, p in enumerate(got):
-        g = ch["segments"][i]
-        assert len(p) == g["len"] and hashlib.sha256(p).hexdigest() == g["sha256"], f"segment {i}"
     steps = []
-    for i, ((t, pi, w), p) in enumerate(zip(segs, got)):
+    for i, (pi, p) in enumerate(zip(pis, got)):
         info = zkl_hip.step_info_for(pi, i, K, i.to_bytes(32, "little"), (i + 1).to_bytes(32, "little"))
         steps.append(zkl_hip.step_proof_encode(pi, info, p))
+    return got, steps
+
+
+def _check_segments(got):
+    ch = _chain()
+    for i, p in enumerate(got):
+        g = ch["segments"][i]
+        assert g["index"] == i and len(p) == g["len"] and hashlib.sha256(p).hexdigest() == g["sha256"], f"segment {i}"
+
+
+@pytest.mark.skipif(_chain() is None, reason="tests/golden/chain_2p16.json not generated")
+def test_chain_program_and_aggregation_match_goldens(oracle, gpu_ctx):
+    """BASELINE configs[2] end to end: the first 8 segments of the synthetic multi-segment
+    program (tests/golden/make_chain_goldens.py), proved on the GPU with 4 contexts in flight,
+    equal the oracle goldens; their zl1 steps aggregate (zkl_agg_prove, FieldExtension::
+    Quadratic) into the golden ZKLRC1 artifact and recursion digest, and into the artifact
+    oracle/agg_ref.py builds from the GPU steps."""
+    import sys
+    import zkl_hip
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import agg_ref
+    ch = _chain()
+    got, steps = _prove_chain(8)
+    _check_segments(got)
     art, dg = zkl_hip.agg_prove(steps)
     ga = ch["aggregation"]
+    assert ga["children"] == 8
     assert len(art) == ga["len"] and hashlib.sha256(art).hexdigest() == ga["sha256"]
     assert dg.hex() == ga["recursion_digest"]
     want, want_dg, _ = agg_ref.agg_prove(oracle, steps)
     assert art == want and dg == want_dg
+    zkl_hip.agg_verify(art)
+
+
+@pytest.mark.skipif(_chain() is None or "aggregation_64" not in _chain() or len(_chain()["segments"]) < 64,
+                    reason="64-segment chain goldens not generated")
+def test_chain_64_segments_and_aggregation_match_goldens(gpu_ctx):
+    """BASELINE configs[3] on one GPU: all 64 segments of the chained program (prove.rs:1018-
+    1050), 4 contexts in flight, equal the 64 oracle goldens; the 64 zl1 steps aggregate
+    (lib.rs:295-551) into the golden 64-child ZKLRC1 artifact (oracle/agg_ref.py over the
+    oracle's step proofs) and recursion digest, and the product verifier accepts it.  The
+    8-GPU run shards exactly these segments (bench.py --gpus 8, zkl_hip/dist.py)."""
+    import zkl_hip
+    ch = _chain()
+    got, steps = _prove_chain(64)
+    _check_segments(got)
+    art, dg = zkl_hip.agg_prove(steps)
+    ga = ch["aggregation_64"]
+    assert ga["children"] == 64
+    assert len(art) == ga["len"] and hashlib.sha256(art).hexdigest() == ga["sha256"]
+    assert dg.hex() == ga["recursion_digest"]
+    zkl_hip.agg_verify(art)
+    T = zkl_hip.agg_trace(steps)
+    assert len(T[0]) == 128  # next_pow2(max(64 + 1, 8)): the padding row (DESIGN.md §10)
+
+
+@pytest.mark.parametrize("log_n,width_flags", [(16, 0), (18, 0), (12, 2)])
+def test_host_trace_chunked_upload_matches_device_entry(gpu_ctx, log_n, width_flags):
+    """zkl_hip_prove_segment with a pageable host trace (column chunks through the pinned ring,
+    each chunk's LDE issued as its DMA lands) gives the proof zkl_hip_prove_segment_device gives
+    for the same trace resident in HBM: chunk sizes of 16 / 4 / 256 columns, widths 204 and 212
+    (the last chunk partial)."""
+    import zkl_hip
+    n = 1 << log_n
+    t, pi, w = zkl_hip.synth_vm_segment(0x5EED0B00 + log_n, log_n, width_flags)
+    opts = zkl_hip.proof_options(w, n, queries=16, grind=4)
+    host = gpu_ctx.prove_segment(t, w, n, pi, opts)
+    assert gpu_ctx.host_times()["upload"] > 0
+    d = gpu_ctx.alloc(w * n * 16)
+    try:
+        gpu_ctx.upload(d, t, w * n * 16)
+        dev = gpu_ctx.prove_segment_device(d, w, n, pi, opts)
+    finally:
+        gpu_ctx.free(d)
+    assert host == dev
+    zkl_hip.verify_segment(host, pi, opts)

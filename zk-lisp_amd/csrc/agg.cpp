@@ -494,8 +494,9 @@ fe fri_paths_agg(const SegmentView& v, fe delta, fe beta) {
   return acc;
 }
 
-// build_agg_trace_from_transcripts (agg/trace.rs:155-693): column-major AGG_W x rows
-std::vector<std::vector<fe>> build_agg_trace(const AggPi& p, const std::vector<Child>& ch) {
+// build_agg_trace_from_transcripts (agg/trace.rs:155-693): column-major AGG_W x rows, in one of
+// the two trace modes of include/zkl_hip.h (ZKL_AGG_TRACE_VALID / ZKL_AGG_TRACE_REFERENCE)
+std::vector<std::vector<fe>> build_agg_trace(const AggPi& p, const std::vector<Child>& ch, uint32_t mode) {
   const size_t nc = ch.size();
   if (nc == 0) throw AggError("AggTrace requires at least one child proof");
   if (p.children_count != nc) throw AggError("AggAirPublicInputs.children_count must match number of children");
@@ -545,10 +546,11 @@ std::vector<std::vector<fe>> build_agg_trace(const AggPi& p, const std::vector<C
   // power-of-two child count >= 8 that leaves no padding row, and the last row then holds the
   // last child's accumulators *before* its increment, so the assertions v_units_acc[last] =
   // v_units_total and child_count_acc[last] = children_count (agg/air.rs:276-304) cannot hold
-  // and no valid aggregation proof exists.  One padding row is always kept here (DESIGN.md
-  // §10); other child counts give the reference's trace length.
+  // and no valid aggregation proof exists.  The valid mode always keeps one padding row
+  // (DESIGN.md §10); other child counts give the reference's trace length.
+  const bool ref = mode == ZKL_AGG_TRACE_REFERENCE;
   size_t rows = 1;
-  while (rows < std::max(nc + 1, MIN_AGG_TRACE_ROWS)) rows *= 2;
+  while (rows < std::max(ref ? nc : nc + 1, MIN_AGG_TRACE_ROWS)) rows *= 2;
   std::vector<std::vector<fe>> T(AGG_W, std::vector<fe>(rows, fe_zero()));
   const fe vm0 = fold_bytes32(p.vm_state_initial), vm1 = fold_bytes32(p.vm_state_final);
   const fe ru0 = fold_bytes32(p.ram_u_initial), ru1 = fold_bytes32(p.ram_u_final);
@@ -575,10 +577,17 @@ std::vector<std::vector<fe>> build_agg_trace(const AggPi& p, const std::vector<C
     T[C_V_UNITS_ACC][i] = v_acc;
     T[C_CHILD_COUNT_ACC][i] = cnt;
     // trace_root_err / constraint_root_err: sum over queries of the root each opening
-    // reproduces minus the committed root; the replay verified every opening against its root
-    // under the library's row-digest rule, so both sums are zero here
-    T[C_TRACE_ROOT_ERR][i] = fe_zero();
-    T[C_CONSTRAINT_ROOT_ERR][i] = fe_zero();
+    // reproduces minus the committed root (agg/trace.rs:553-600).  The valid mode: the replay
+    // verified every opening against its root under the library's row-digest rule, so both
+    // sums are zero.  The reference mode rebuilds each leaf with
+    // hash_row_poseidon (agg/child.rs:1025-1045) and each path from the batch proof with those
+    // leaves (into_openings); every path of one batch then ends on the same root, so the sum
+    // is num_queries x (that root - the committed root), roots folded by fold_bytes32_to_fe
+    // (the digest value itself).
+    const fe nq{(uint64_t)ch[i].v.positions.size(), 0};
+    T[C_TRACE_ROOT_ERR][i] = ref ? fe_mul(nq, fe_sub(ch[i].v.trace_root_ref, ch[i].v.trace_root)) : fe_zero();
+    T[C_CONSTRAINT_ROOT_ERR][i] =
+        ref ? fe_mul(nq, fe_sub(ch[i].v.constraint_root_ref, ch[i].v.constraint_root)) : fe_zero();
     T[C_VM_CHAIN_ERR][i] = vm_err;
     T[C_RAM_U_CHAIN_ERR][i] = ru_err;
     T[C_RAM_S_CHAIN_ERR][i] = rs_err;
@@ -653,7 +662,10 @@ void agg_transition(const T* c, const T* nx, T is_last, T r[AGG_TC]) {
   r[23] = c[C_ROM_CHAIN_ERR_2];
 }
 
-struct AggOpts { uint32_t queries, blowup, grind, field_ext; };
+struct AggOpts {
+  uint32_t queries, blowup, grind, field_ext;
+  bool check_air = true;  // reject a trace that violates ZlAggAir (off in ZKL_AGG_TRACE_REFERENCE mode)
+};
 
 // winterfell 0.13.1 Prover::prove for ZlAggAir over E = QuadExtension<f128> (or E = f128 when
 // the security target is below 128 bits: FieldExtension::None, prove.rs:647-651)
@@ -700,8 +712,9 @@ std::vector<uint8_t> prove_air(const std::vector<std::vector<fe>>& trace, const 
 
   // 0. the trace must satisfy the AIR (winterfell validates this in debug builds; the
   // composition degree bound C n equals the CE domain here, so a violated constraint would
-  // otherwise only surface as a proof the verifier rejects)
-  {
+  // otherwise only surface as a proof the verifier rejects).  The reference-trace mode proves
+  // whatever trace the reference builds, as its release prover does.
+  if (ao.check_air) {
     std::vector<fe> cur(W), nxt(W);
     fe tc[AGG_TC];
     for (size_t i = 0; i + 1 < n; i++) {  // one transition exemption: the last row is not checked
@@ -1358,10 +1371,12 @@ int zkl_agg_prove(const uint8_t* const* steps, const size_t* step_lens, uint32_t
   const int rc = guarded_call([&] {
     const std::vector<Child> ch = load_children(steps, step_lens, n_steps);
     const AggPi pi = public_of(ch);  // build_public; prove() re-derives suite / count / ms identically
-    const auto T = build_agg_trace(pi, ch);
+    const auto T = build_agg_trace(pi, ch, opts->trace_mode);
     AggOpts ao{std::max<uint32_t>(opts->queries, 16), opts->blowup, opts->grind,
                opts->min_security_bits >= 128 ? 2u : 1u};
     if (ao.queries > 255) throw AggError("queries must be at most 255");
+    if (ao.grind > 32) throw AggError("grinding factor must be at most 32");  // ProofOptions::new [WF-recall]
+    if (opts->trace_mode > ZKL_AGG_TRACE_REFERENCE) throw AggError("unknown aggregation trace mode");
     if (opts->min_security_bits >= 64) {  // prove.rs:664-681
       if (conjectured_bits(ao.queries, ao.blowup, ao.grind, ao.field_ext) < opts->min_security_bits)
         throw AggError(
@@ -1369,6 +1384,7 @@ int zkl_agg_prove(const uint8_t* const* steps, const size_t* step_lens, uint32_t
             "or lower --security-bits");
     }
     const std::vector<fe> el = agg_pi_elements(pi);
+    ao.check_air = opts->trace_mode == ZKL_AGG_TRACE_VALID;
     const std::vector<uint8_t> proof =
         ao.field_ext == 2 ? prove_air<fe2>(T, el, pi, ao) : prove_air<fe>(T, el, pi, ao);
     art = encode_artifact(pi, proof);
@@ -1392,10 +1408,15 @@ int zkl_agg_verify(const uint8_t* artifact, size_t len, uint32_t min_security_bi
 
 int zkl_agg_trace(const uint8_t* const* steps, const size_t* step_lens, uint32_t n_steps, zkl_f128* out,
                   uint32_t max_rows, uint32_t* rows_out) {
-  if (!rows_out) return ZKL_E_INVALID;
+  return zkl_agg_trace_mode(steps, step_lens, n_steps, ZKL_AGG_TRACE_VALID, out, max_rows, rows_out);
+}
+
+int zkl_agg_trace_mode(const uint8_t* const* steps, const size_t* step_lens, uint32_t n_steps, uint32_t trace_mode,
+                       zkl_f128* out, uint32_t max_rows, uint32_t* rows_out) {
+  if (!rows_out || trace_mode > ZKL_AGG_TRACE_REFERENCE) return ZKL_E_INVALID;
   return guarded_call([&] {
     const std::vector<Child> ch = load_children(steps, step_lens, n_steps);
-    const auto T = build_agg_trace(public_of(ch), ch);
+    const auto T = build_agg_trace(public_of(ch), ch, trace_mode);
     const uint32_t rows = (uint32_t)T[0].size();
     *rows_out = rows;
     if (!out) return;

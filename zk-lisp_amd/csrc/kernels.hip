@@ -30,7 +30,9 @@ void upload_alphas_from_device(ProofConsts* dK, const fe* d, int n, hipStream_t 
 }
 static void limbs26(fe a, uint32_t l[5]);
 void upload_deep_coeffs(ProofConsts* dK, const fe* h, int n, hipStream_t s) {
-  if (n > 512) throw std::invalid_argument("more than 512 DEEP coefficients");
+  // deep_kernel's unreduced 64-bit digit columns stay below the 2^62 REDC bound for at most 256
+  // terms (column 3 takes four 26 x 26-bit products per term, < 2^54)
+  if (n > 256) throw std::invalid_argument("more than 256 DEEP coefficients (W + C)");
   ZKL_HIPCHECK(hipMemcpyAsync(dK->deep, h, sizeof(fe) * n, hipMemcpyHostToDevice, s));
   static thread_local std::vector<uint32_t> m;
   m.assign((size_t)n * 5, 0);
@@ -1494,7 +1496,8 @@ void launch_ood(const OodArgs& A, fe* d_partial, hipStream_t s) {
 //   = [(S(x) - S(z)) (x - zg) + (S(x) - S(zg)) (x - z)] / ((x - z)(x - zg)),  S = sum_i g_i T_i.
 // S(x) is one lazily reduced dot product per point: the coefficients as Montgomery limbs
 // (g R, uniform -> SGPR operands), each column value split into 26-bit limbs, 25
-// v_mad_u64_u32 per column into 64-bit columns (211 terms of < 2^54 stay below 2^64) and a
+// v_mad_u64_u32 per column into 64-bit columns (up to 256 terms of < 2^54 stay below the 2^62
+// the REDC needs; upload_deep_coeffs enforces it, W + C <= 226 here) and a
 // single REDC.  Each thread takes DEEP_PTS points T apart (coalesced), keeps
 // DEEP_COLS x DEEP_PTS loads in flight, and shares one inversion among its points.
 // points per thread: 2 keeps the kernel at 96 VGPRs (5 waves per SIMD, more loads in flight;

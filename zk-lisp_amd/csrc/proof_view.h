@@ -58,7 +58,18 @@ struct SegmentView {
   std::vector<std::vector<size_t>> fri_positions;  // per layer: folded positions (order of first use)
   std::vector<std::vector<fe>> fri_values;         // per layer: [e_y, e_{y+h}] per folded position
   std::vector<fe> remainder;                       // reversed coefficients, degree <= rem_deg
+  // the roots the trace / constraint openings reproduce when each opened row is hashed as the
+  // reference's hash_row_poseidon does (agg/child.rs:1025-1045: a one-chunk row is not merged)
+  // and the batch proof is decompressed with those leaves; equal to trace_root /
+  // constraint_root unless a row is one chunk narrower than its partition
+  fe trace_root_ref{}, constraint_root_ref{};
 };
+
+// ProofOptions bounds winterfell enforces when it builds or reads options (ProofOptions::new
+// [WF-recall]): queries 1..255, blowup a power of two in 2..128, grinding <= 32, folding 2,
+// remainder degree 2^k - 1 below the blowup, partitions 1..16, hash rate 1..255.  "" or the
+// first violated bound.
+std::string check_proof_options(const zkl_proof_options& o);
 
 // Parses and verifies one segment proof under the given public inputs and options (the
 // options must equal those recorded in the proof).  Returns "" when the proof verifies, the

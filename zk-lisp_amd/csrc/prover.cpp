@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <atomic>
 #include <algorithm>
 #include <chrono>
 #include <functional>
@@ -13,6 +14,7 @@
 #include <memory>
 #include <mutex>
 #include <set>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -101,6 +103,14 @@ struct zkl_ctx {
   HBuf h_asrt, h_ood, h_addr, h_gv;  // pinned staging: assertions, OOD partial sums, gather plan/values
   hipStream_t aux = nullptr;         // copy stream: assertion upload overlapped with the trace commitment
   hipEvent_t aux_ev = nullptr, hev = nullptr;
+  // host-trace upload (zkl_hip_prove_segment): a ring of pinned slots, each filled from the
+  // caller's pageable trace by host threads and DMA'd on its own copy stream while the compute
+  // stream transforms the columns that already landed
+  hipStream_t up = nullptr;
+  std::vector<void*> up_slot;
+  std::vector<hipEvent_t> up_ev;
+  size_t up_slot_bytes = 0;
+  double up_ms = 0;  // host wall time of the last proof's upload loop
   hipEvent_t stage_ev[ZKL_NUM_STAGES + 1] = {};
   bool stage_ev_ready = false;
   size_t pert_key_n = 0, pert_key_ce = 0;
@@ -269,19 +279,89 @@ void validate_request(uint32_t W, uint32_t n32, const zkl_air_public_inputs& pi,
   if (o.field_extension != 1) throw InvalidArg("only FieldExtension::None is supported for segment proofs");
   if (o.fri_folding_factor != 2) throw InvalidArg("only FRI folding factor 2 is supported");
   if (o.batching_constraints != 0 || o.batching_deep != 0) throw InvalidArg("only BatchingMethod::Linear is supported");
+  // winterfell ProofOptions::new bounds [WF-recall]: blowup a power of two in 2..=128, grinding
+  // factor <= 32 (the proof's context stores both as u8; a grind above 64 could never be met)
   if (o.blowup_factor < 2 || (o.blowup_factor & (o.blowup_factor - 1))) throw InvalidArg("blowup must be a power of two");
+  if (o.blowup_factor > 128) throw InvalidArg("blowup must be at most 128");
+  if (o.grinding_factor > 32) throw InvalidArg("grinding_factor must be at most 32");
   if (o.num_queries == 0 || o.num_queries > 255) throw InvalidArg("num_queries must be in 1..255");
   // winter-air PartitionOptions::new bounds (num_partitions 1..=16, min_partition_size 1..=256)
   if (o.num_partitions < 1 || o.num_partitions > 16) throw InvalidArg("num_partitions must be in 1..16");
-  if (o.hash_rate < 1 || o.hash_rate > 256) throw InvalidArg("hash_rate must be in 1..256");
+  if (o.hash_rate < 1 || o.hash_rate > 255) throw InvalidArg("hash_rate must be in 1..255 (a u8 in the proof context)");
   if (o.fri_remainder_max_degree > 15 || ((o.fri_remainder_max_degree + 1) & o.fri_remainder_max_degree))
     throw InvalidArg("fri_remainder_max_degree must be one less than a power of two, at most 15");
   if (pi.n_main_slots > ZKL_MAX_MAIN_SLOTS) throw InvalidArg("n_main_slots exceeds ZKL_MAX_MAIN_SLOTS");
   if (W == 0 || W > 4096) throw InvalidArg("trace width must be in 1..4096");
 }
 
+// Host-resident trace -> coefficient buffer, column chunk by column chunk, with the trace LDE of
+// each chunk (iNTT over <g>, coset shift, DIT evaluation, all per-column transforms) issued on
+// the compute stream as soon as its DMA lands.  The caller's trace is pageable memory (the Rust
+// binding passes its Vec): host threads copy each chunk into a pinned slot (ZKL_UP_SLOTS slots of
+// ZKL_UP_SLOT_MB), the copy stream DMAs the slot, the compute stream waits on that copy's event.
+// The PCIe upload thus overlaps the LDE of the chunks before it, and the host copy of chunk j+1
+// overlaps the DMA of chunk j.
+constexpr int UP_SLOTS = 4;
+constexpr size_t UP_SLOT_BYTES = (size_t)16 << 20;
+
+void parallel_copy(void* dst, const void* src, size_t bytes, unsigned nt) {
+  if (nt <= 1 || bytes < ((size_t)1 << 20)) { memcpy(dst, src, bytes); return; }
+  const size_t per = ((bytes + nt - 1) / nt + 63) & ~(size_t)63;
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nt && t * per < bytes; t++)
+    th.emplace_back([=] { memcpy((char*)dst + t * per, (const char*)src + t * per, std::min(per, bytes - t * per)); });
+  memcpy(dst, src, std::min(per, bytes));
+  for (auto& x : th) x.join();
+}
+
+template <class F>
+void upload_trace_chunked(zkl_ctx* C, const void* h_trace, uint32_t W, size_t n, hipStream_t s, F&& on_chunk) {
+  if (!C->up) {
+    HIPCHECK(hipStreamCreateWithFlags(&C->up, hipStreamNonBlocking));
+    C->up_slot.assign(UP_SLOTS, nullptr);
+    C->up_ev.assign(UP_SLOTS, nullptr);
+    for (int k = 0; k < UP_SLOTS; k++) {
+      HIPCHECK(hipHostMalloc(&C->up_slot[k], UP_SLOT_BYTES, hipHostMallocDefault));
+      HIPCHECK(hipEventCreateWithFlags(&C->up_ev[k], hipEventDisableTiming));
+    }
+    C->up_slot_bytes = UP_SLOT_BYTES;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t col_bytes = n * sizeof(fe);
+  const uint32_t per = (uint32_t)std::max<size_t>(1, C->up_slot_bytes / col_bytes);
+  const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency() / 2));
+  bool used[UP_SLOTS] = {false, false, false, false};
+  int k = 0;
+  for (uint32_t c0 = 0; c0 < W; c0 += per, k = (k + 1) % UP_SLOTS) {
+    const uint32_t nc = std::min(per, W - c0);
+    if (col_bytes * nc > C->up_slot_bytes) {  // one column larger than a slot: plain pageable copy
+      HIPCHECK(hipMemcpyAsync(C->coef.f() + (size_t)c0 * n, (const char*)h_trace + c0 * col_bytes, col_bytes * nc,
+                              hipMemcpyHostToDevice, s));
+      on_chunk(c0, nc);
+      continue;
+    }
+    if (used[k]) HIPCHECK(hipEventSynchronize(C->up_ev[k]));  // the slot's previous DMA has read it
+    parallel_copy(C->up_slot[k], (const char*)h_trace + c0 * col_bytes, col_bytes * nc, nt);
+    HIPCHECK(hipMemcpyAsync(C->coef.f() + (size_t)c0 * n, C->up_slot[k], col_bytes * nc, hipMemcpyHostToDevice, C->up));
+    HIPCHECK(hipEventRecord(C->up_ev[k], C->up));
+    used[k] = true;
+    HIPCHECK(hipStreamWaitEvent(s, C->up_ev[k], 0));
+    on_chunk(c0, nc);
+  }
+  C->up_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// proofs running in any context: the row-digest rule (a process-wide test switch, DESIGN.md
+// §3.1) may only change while this is zero
+std::atomic<int> g_proofs_in_flight{0};
+struct InFlight {
+  InFlight() { g_proofs_in_flight.fetch_add(1); }
+  ~InFlight() { g_proofs_in_flight.fetch_sub(1); }
+};
+
 void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t W, uint32_t n32,
                 const zkl_air_public_inputs& pi, const zkl_proof_options& o, std::vector<uint8_t>& out) {
+  const InFlight in_flight;
   const auto t_call0 = std::chrono::steady_clock::now();
   hipStream_t s = C->stream;
   const size_t n = n32;
@@ -305,13 +385,21 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   // ---- 1. trace LDE (DefaultTraceLde::new): iNTT over <g>, coset LDE over 3*<w_N>
   C->coef.ensure((size_t)W * n * sizeof(fe));
   C->lde.ensure((size_t)W * N * sizeof(fe));
-  HIPCHECK(hipMemcpyAsync(C->coef.p, d_trace_in, (size_t)W * n * sizeof(fe),
-                          trace_on_host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, s));
-  {
+  // columns [c0, c0 + nc): iNTT -> n*coef bit-reversed, scale c_k * 3^k (coset shift), DIT
+  auto lde_cols = [&](uint32_t c0, uint32_t nc) {
+    fe* cf = C->coef.f() + (size_t)c0 * n;
+    launch_ntt_stages(cf, nc, n, true, 0, logn - 1, miroots, Ntab, s);
+    launch_scale_bitrev(cf, nc, n, C->opow_n.f(), s);
+    launch_lde_from_coeffs(cf, nc, n, N, mroots, Ntab, C->lde.f() + (size_t)c0 * N, s);
+  };
+  if (trace_on_host) {
     KScope k(C, KF_NTT);
-    launch_ntt_stages(C->coef.f(), W, n, true, 0, logn - 1, miroots, Ntab, s);  // -> n*coef, bit-reversed
-    launch_scale_bitrev(C->coef.f(), W, n, C->opow_n.f(), s);                  // -> c_k * 3^k (coset shift)
-    launch_lde_from_coeffs(C->coef.f(), W, n, N, mroots, Ntab, C->lde.f(), s);
+    upload_trace_chunked(C, d_trace_in, W, n, s, lde_cols);
+  } else {
+    C->up_ms = 0;
+    HIPCHECK(hipMemcpyAsync(C->coef.p, d_trace_in, (size_t)W * n * sizeof(fe), hipMemcpyDeviceToDevice, s));
+    KScope k(C, KF_NTT);
+    lde_cols(0, W);
   }
   check_launch("trace LDE");
   T.mark(1);
@@ -856,6 +944,12 @@ void zkl_hip_destroy(zkl_ctx* c) {
   (void)hipStreamDestroy(c->stream);
   if (c->stage_ev_ready)
     for (auto& e : c->stage_ev) (void)hipEventDestroy(e);
+  if (c->up) {
+    (void)hipStreamSynchronize(c->up);
+    (void)hipStreamDestroy(c->up);
+    for (void* p : c->up_slot) (void)hipHostFree(p);
+    for (hipEvent_t e : c->up_ev) (void)hipEventDestroy(e);
+  }
   if (c->aux) {
     (void)hipStreamSynchronize(c->aux);
     (void)hipStreamDestroy(c->aux);
@@ -926,8 +1020,9 @@ int zkl_verify_segment(const uint8_t* proof, size_t len, const zkl_air_public_in
 
 int zkl_hip_host_times(const zkl_ctx* c, double* out_ms, int max_n) {
   if (!c || !out_ms) return ZKL_E_INVALID;
-  int k = std::min(max_n, 3);
-  for (int i = 0; i < k; i++) out_ms[i] = c->host_ms[i];
+  const double v[4] = {c->host_ms[0], c->host_ms[1], c->host_ms[2], c->up_ms};
+  const int k = std::min(max_n, 4);
+  for (int i = 0; i < k; i++) out_ms[i] = v[i];
   return k;
 }
 
@@ -1045,6 +1140,10 @@ int zkl_hip_set_ntt_mode(int lazy) {
 
 int zkl_hip_set_row_digest_rule(int rule) {
   if (rule < 0 || rule > 1) return ZKL_E_INVALID;
+  if (g_proofs_in_flight.load() != 0) {
+    set_err(nullptr, "the row-digest rule cannot change while a proof is in flight");
+    return ZKL_E_INVALID;
+  }
   set_row_digest_rule(rule);
   return 0;
 }

@@ -156,14 +156,35 @@ size_t partition_size(uint32_t np, uint32_t rate, size_t ncols) {
   return std::max<size_t>(a, rate);
 }
 
-// row digest of commit_to_rows under the library's one-chunk rule (kernels.h row_digest_rule)
-fe row_digest(const fe* row, size_t ncols, size_t psize) {
+// row digest of commit_to_rows under a one-chunk rule (0: winterfell, 1: hash_row_poseidon of
+// agg/child.rs:1025-1045)
+fe row_digest_rule_n(const fe* row, size_t ncols, size_t psize, int rule) {
   const Hasher& H = hasher();
   if (psize == ncols) return H.hash_elements(row, ncols);
   std::vector<fe> d;
   for (size_t s = 0; s < ncols; s += psize) d.push_back(H.hash_elements(row + s, std::min(psize, ncols - s)));
-  if (d.size() == 1 && row_digest_rule() == 1) return d[0];
+  if (d.size() == 1 && rule == 1) return d[0];
   return H.merge_many(d.data(), d.size());
+}
+// ... under the library's rule (kernels.h row_digest_rule)
+fe row_digest(const fe* row, size_t ncols, size_t psize) {
+  return row_digest_rule_n(row, ncols, psize, row_digest_rule());
+}
+
+// the root a batch opening reproduces with hash_row_poseidon leaves (SegmentView::*_root_ref);
+// `proof` is a copy of the opening's reader taken before it was consumed
+fe reference_rule_root(Rd proof, size_t N, const std::vector<size_t>& pos, const std::vector<fe>& rows, size_t ncols,
+                       size_t psize, const std::vector<fe>& leaves, fe committed) {
+  std::vector<fe> l1(pos.size());
+  bool same = true;
+  for (size_t k = 0; k < pos.size(); k++) {
+    l1[k] = row_digest_rule_n(&rows[k * ncols], ncols, psize, 1);
+    same = same && fe_eq(l1[k], leaves[k]);
+  }
+  if (same) return committed;
+  fe root{};
+  if (!batch_merkle_root(proof, N, pos, l1, &root)) return committed;  // malformed: rejected by the caller
+  return root;
 }
 
 int ilog2z(size_t n) { int k = 0; while (((size_t)1 << k) < n) k++; return k; }
@@ -180,6 +201,21 @@ fe transition_sum(const AirInstance& air, const std::vector<fe>& cur, const std:
 }
 
 }  // namespace
+
+std::string check_proof_options(const zkl_proof_options& o) {
+  const auto pow2 = [](uint32_t x) { return x && !(x & (x - 1)); };
+  if (o.num_queries < 1 || o.num_queries > 255) return "number of queries must be in 1..255";
+  if (!pow2(o.blowup_factor) || o.blowup_factor < 2 || o.blowup_factor > 128)
+    return "blowup factor must be a power of two in 2..128";
+  if (o.grinding_factor > 32) return "grinding factor must be at most 32";
+  if (o.field_extension < 1 || o.field_extension > 3) return "unknown field extension";
+  if (o.fri_folding_factor != 2) return "FRI folding factor must be 2";
+  if (!pow2(o.fri_remainder_max_degree + 1) || o.fri_remainder_max_degree >= o.blowup_factor)
+    return "FRI remainder degree must be 2^k - 1 below the blowup factor";
+  if (o.num_partitions < 1 || o.num_partitions > 16) return "number of partitions must be in 1..16";
+  if (o.hash_rate < 1 || o.hash_rate > 255) return "hash rate must be in 1..255";
+  return "";
+}
 
 std::string verify_segment(const uint8_t* proof, size_t len, const zkl_air_public_inputs& pi,
                            const zkl_proof_options& opts, SegmentView* out) {
@@ -216,6 +252,10 @@ std::string verify_segment_ex(const uint8_t* proof, size_t len, const zkl_air_pu
   const zkl_proof_options opts = po;
   const size_t nq_proof = r.u8();
   if (r.bad) return "truncated context";
+  {
+    const std::string e = check_proof_options(opts);  // options decoded from the proof (winterfell reads them so)
+    if (!e.empty()) return "proof options: " + e;
+  }
   if (logn < 5 || logn > 30) return "trace length out of range";
   if (opts.field_extension != 1 || opts.fri_folding_factor != 2) return "unsupported proof options";
   const size_t n = (size_t)1 << logn, N = n * opts.blowup_factor;
@@ -365,14 +405,17 @@ std::string verify_segment_ex(const uint8_t* proof, size_t len, const zkl_air_pu
   {
     std::vector<fe> leaves(nq);
     fe root;
+    const Rd tq_p0 = tq_p, cq_p0 = cq_p;
     size_t ps = partition_size(opts.num_partitions, opts.hash_rate, W);
     for (size_t k = 0; k < nq; k++) leaves[k] = row_digest(&V.trace_rows[k * W], W, ps);
     if (!batch_merkle_root(tq_p, N, pos, leaves, &root) || !fe_eq(root, V.trace_root) || !tq_p.done())
       return "trace Merkle opening does not reproduce the trace commitment";
+    V.trace_root_ref = reference_rule_root(tq_p0, N, pos, V.trace_rows, W, ps, leaves, V.trace_root);
     ps = partition_size(opts.num_partitions, opts.hash_rate, (size_t)C);
     for (size_t k = 0; k < nq; k++) leaves[k] = row_digest(&V.comp_rows[k * C], (size_t)C, ps);
     if (!batch_merkle_root(cq_p, N, pos, leaves, &root) || !fe_eq(root, V.constraint_root) || !cq_p.done())
       return "constraint Merkle opening does not reproduce the constraint commitment";
+    V.constraint_root_ref = reference_rule_root(cq_p0, N, pos, V.comp_rows, (size_t)C, ps, leaves, V.constraint_root);
   }
 
   // ---- DEEP composition at the query positions

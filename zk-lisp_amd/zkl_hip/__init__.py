@@ -167,6 +167,8 @@ def load_library():
                                   P(C.c_size_t), C.c_void_p]
     lib.zkl_agg_verify.argtypes = [C.c_char_p, C.c_size_t, C.c_uint32]
     lib.zkl_agg_trace.argtypes = [P(C.c_char_p), P(C.c_size_t), C.c_uint32, C.c_void_p, C.c_uint32, P(C.c_uint32)]
+    lib.zkl_agg_trace_mode.argtypes = [P(C.c_char_p), P(C.c_size_t), C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32,
+                                       P(C.c_uint32)]
     _lib = lib
     return lib
 
@@ -174,7 +176,11 @@ def load_library():
 class AggOptions(C.Structure):
     """zk_lisp_proof::ProverOptions as the aggregation reads it (zk-lisp-proof/src/lib.rs:40-66)."""
     _fields_ = [("queries", C.c_uint32), ("blowup", C.c_uint32), ("grind", C.c_uint32),
-                ("min_security_bits", C.c_uint32)]
+                ("min_security_bits", C.c_uint32), ("trace_mode", C.c_uint32)]
+
+
+AGG_TRACE_VALID = 0      # ZKL_AGG_TRACE_VALID: one padding row, zero root errors (proof.bin)
+AGG_TRACE_REFERENCE = 1  # ZKL_AGG_TRACE_REFERENCE: agg/trace.rs's own trace bytes (DESIGN.md §10)
 
 
 def _steps_args(steps):
@@ -183,12 +189,12 @@ def _steps_args(steps):
     return arr, lens
 
 
-def agg_prove(steps, queries=64, blowup=16, grind=16, min_security_bits=128):
+def agg_prove(steps, queries=64, blowup=16, grind=16, min_security_bits=128, trace_mode=AGG_TRACE_VALID):
     """RecursionPublicBuilder::build_public + RecursionBackend::prove + RecursionArtifactCodec::
     encode (lib.rs:295-551): ZKLSTP1 step proofs -> (ZKLRC1 artifact, recursion digest)."""
     lib = load_library()
     arr, lens = _steps_args(steps)
-    o = AggOptions(queries, blowup, grind, min_security_bits)
+    o = AggOptions(queries, blowup, grind, min_security_bits, trace_mode)
     out, ln, dg = C.POINTER(C.c_uint8)(), C.c_size_t(), (C.c_uint8 * 32)()
     rc = lib.zkl_agg_prove(arr, lens, len(steps), C.byref(o), C.byref(out), C.byref(ln), dg)
     if rc:
@@ -207,16 +213,17 @@ def agg_verify(artifact: bytes, min_security_bits: int = 128) -> None:
         raise ZklError(rc, lib.zkl_hip_last_error(None).decode(errors="replace"))
 
 
-def agg_trace(steps):
+def agg_trace(steps, trace_mode=AGG_TRACE_VALID):
     """build_agg_trace_from_transcripts (agg/trace.rs:155-238): 31 column lists of ints."""
     lib = load_library()
     arr, lens = _steps_args(steps)
     rows = C.c_uint32()
-    rc = lib.zkl_agg_trace(arr, lens, len(steps), None, 0, C.byref(rows))
+    rc = lib.zkl_agg_trace_mode(arr, lens, len(steps), trace_mode, None, 0, C.byref(rows))
     if rc:
         raise ZklError(rc, lib.zkl_hip_last_error(None).decode(errors="replace"))
     buf = (F128 * (31 * rows.value))()
-    rc = lib.zkl_agg_trace(arr, lens, len(steps), C.cast(buf, C.c_void_p), rows.value, C.byref(rows))
+    rc = lib.zkl_agg_trace_mode(arr, lens, len(steps), trace_mode, C.cast(buf, C.c_void_p), rows.value,
+                                C.byref(rows))
     if rc:
         raise ZklError(rc, lib.zkl_hip_last_error(None).decode(errors="replace"))
     r = rows.value
@@ -258,12 +265,19 @@ def parse_agg_artifact(b: bytes) -> dict:
 
 
 def step_info_for(pi: AirPublicInputs, index: int, total: int, state_in: bytes, state_out: bytes,
-                  lambda_bits: int = 128) -> "StepInfo":
+                  lambda_bits: int = 128, main_args=()) -> "StepInfo":
     """zl1 step metadata as prove_segment fills it (prove.rs:1103-1174): suite = program_id
     (prove.rs:985), the segment boundary bytes fe_to_bytes_fold of the AIR public inputs'
-    pc_init / RAM grand products / ROM lanes (SegmentBoundaryBytes, prove.rs:1112), and the VM
-    state hashes of the trace builder (here given)."""
+    pc_init / RAM grand products / ROM lanes (SegmentBoundaryBytes, prove.rs:1112), the VM
+    state hashes of the trace builder (here given) and the program's typed main args (the
+    PublicInputs::main_args the zl1 proof carries; ints or (tag, bytes) as build_trace takes)."""
     info = StepInfo()
+    if len(main_args) > 8:
+        raise ValueError("at most 8 main args")
+    info.n_main_args = len(main_args)
+    va = _vm_args(list(main_args))
+    for i in range(len(main_args)):
+        info.main_args[i] = va[i]
     info.suite_id[:] = bytes(pi.program_id)
     info.lambda_bits, info.segment_index, info.segments_total = lambda_bits, index, total
 
@@ -520,10 +534,10 @@ class Context:
         return dict(zip(STAGE_NAMES[:k], list(arr)[:k]))
 
     def host_times(self):
-        """{setup, host_unoverlapped, call} wall ms of the last proof (host side)."""
-        arr = (C.c_double * 3)()
-        k = self.lib.zkl_hip_host_times(self.ptr, arr, 3)
-        return dict(zip(("setup", "host_unoverlapped", "call"), list(arr)[:k]))
+        """{setup, host_unoverlapped, call, upload} wall ms of the last proof (host side)."""
+        arr = (C.c_double * 4)()
+        k = self.lib.zkl_hip_host_times(self.ptr, arr, 4)
+        return dict(zip(("setup", "host_unoverlapped", "call", "upload"), list(arr)[:k]))
 
     def kernel_times(self):
         """{family: (ms, launches)} of the last proof, from HIP events on the ctx stream."""
