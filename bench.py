@@ -153,15 +153,25 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_threads(requested):
-    """Threads of the CPU baseline: every core this process may run on (sched_getaffinity;
-    BASELINE.md §2: the host's cores), unless --cpu-threads says otherwise."""
-    if requested:
-        return requested
+def cpu_affinity():
     try:
         return len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         return os.cpu_count() or 1
+
+
+def cpu_threads(requested):
+    """Threads of the CPU baseline: the CPUs this process can actually use -- the cores it may
+    run on (sched_getaffinity) capped by the cgroup's CPU quota (cpu.max).  On the GPU box the
+    affinity mask lists every core of the host (256 on the EPYC 9575F node) while the quota
+    grants 16 CPUs' worth of time; one proof on 256 threads there measured 96.9 s against
+    ~37 s on 16 (profiles/r03/cpu_baseline_threads.json), so the quota is the core count the
+    host gives this run.  --cpu-threads overrides."""
+    if requested:
+        return requested
+    n = cpu_affinity()
+    q = cgroup_cpu_quota()
+    return max(1, min(n, int(q))) if q else n
 
 
 def cgroup_cpu_quota():
@@ -193,7 +203,7 @@ def cpu_baseline(log_n, threads, gpu_proof, log_n_target):
                        "grind", "queries"), (round(x / 1e3, 3) for x in orc.last_times())))
     orc.set_threads(1)
     out = {"unit": "segment-proofs/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
-           "cores_available": cpu_threads(0), "cgroup_cpu_quota": cgroup_cpu_quota(),
+           "cores_in_affinity_mask": cpu_affinity(), "cgroup_cpu_quota": cgroup_cpu_quota(),
            "mode": "one proof using every thread (row hashing, Merkle levels, LDE columns, constraint "
                    "evaluation, DEEP and grinding split over the threads)",
            "sample_seconds": round(dt, 2), "stage_seconds": stages}
@@ -395,22 +405,30 @@ def step_info(zkl_hip, pi, index, total):
     return info
 
 
-def handoff(zkl_hip, dist, items, total, chained=False):
+def handoff(zkl_hip, dist, items, total, chained=False, device=0):
     """Aggregation hand-off: each rank wraps its proofs as zl1 steps (ZKLSTP1),
-    rank 0 gathers, orders and chain-checks them and forms the children root the aggregation
-    proof commits to (agg/child.rs:853-895).  Returns (summary, ordered step bytes) on rank 0."""
+    rank 0 gathers them over RCCL (zkl_comm_gather_bytes: lengths all-gathered, then one
+    ncclSend per rank to the root over xGMI), orders and chain-checks them and forms the
+    children root the aggregation proof commits to (agg/child.rs:853-895).  If RCCL cannot
+    start on every rank the gather runs over gloo and the line says why.  Returns (summary,
+    ordered step bytes) on rank 0."""
+    comm, cerr = dist.init_rccl(device)
     t_h = time.perf_counter()
     enc = [chain_step(zkl_hip, i, total, pi, proof) if chained else
            zkl_hip.step_proof_encode(pi, step_info(zkl_hip, pi, i, total), proof) for i, pi, proof in items]
-    steps = dist.collect_step_proofs(enc)
+    steps = dist.collect_step_proofs(enc, comm)
     if steps is None:
         return None, None
     root = zkl_hip.children_root(bytes(steps[0]["program_id"]), [d["digest"] for d in steps],
                                  [d["root_trace"] for d in steps])
-    return ({"segments": len(steps), "step_bytes": sum(d["bytes"] for d in steps),
-             "ms": round((time.perf_counter() - t_h) * 1e3, 2), "children_root": root[:16].hex(),
-             "transport": "gloo (host bytes; the proofs already live in host memory)"},
-            [d["raw"] for d in steps])
+    out = {"segments": len(steps), "step_bytes": sum(d["bytes"] for d in steps),
+           "ms": round((time.perf_counter() - t_h) * 1e3, 2), "children_root": root[:16].hex()}
+    if comm is not None:
+        out["transport"] = "rccl (ncclAllGather of lengths + ncclSend/ncclRecv to rank 0)"
+        out["rccl_device_ms"] = round(comm.last_ms(), 3)
+    else:
+        out["transport"] = f"gloo (RCCL unavailable: {cerr})"
+    return out, [d["raw"] for d in steps]
 
 
 def main():
@@ -539,7 +557,7 @@ def main():
                      "parity": parity_of(hp, seed, log_n)["golden"], "two_contexts_in_flight": inflight2}
     del trace
     ctx.close()
-    hand, _ = handoff(zkl_hip, dist, [(rank, pi, proof)], world)
+    hand, _ = handoff(zkl_hip, dist, [(rank, pi, proof)], world, device=device)
 
     # configs[3] shape: S distinct segments sharded over the ranks, pipelined per rank
     c4 = None
@@ -555,7 +573,7 @@ def main():
         items = pl.proofs()
         par4 = dist.gather_to_root([chain_parity(i, p) for i, _, p in items])
         pl.close()
-        h4, steps4 = handoff(zkl_hip, dist, items, n_seg, chained=True)
+        h4, steps4 = handoff(zkl_hip, dist, items, n_seg, chained=True, device=device)
         if rank == 0:
             flat = [g for r in par4 for g in r]
             c4 = {"config": f"BASELINE configs[3] shape: a {n_seg}-segment synthetic program (2^{log_n}-row segments, "

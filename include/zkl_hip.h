@@ -400,6 +400,32 @@ int zkl_agg_trace(const uint8_t* const* steps, const size_t* step_lens, uint32_t
 int zkl_agg_trace_mode(const uint8_t* const* steps, const size_t* step_lens, uint32_t n_steps,
                        uint32_t trace_mode, zkl_f128* out, uint32_t max_rows, uint32_t* rows_out);
 
+/* ---- multi-GPU boundary exchange --------------------------
+ * One process per GPU proves its own segments; the step proofs (zl1 ZKLSTP1 bytes with the
+ * boundary fields the aggregation chains: state hashes, RAM grand products, ROM lanes) are
+ * gathered on the aggregating rank with RCCL point-to-point transfers over xGMI.  Replaces the
+ * reference's in-process Vec<StepProof> hand-off (prove.rs:1018-1050 -> lib.rs:382-482).
+ * RCCL is opened at run time; without it these calls fail with ZKL_E_INVALID and
+ * zkl_hip_last_error(NULL) says why (the single-GPU path does not need it). */
+typedef struct zkl_comm zkl_comm;
+/* ZKL_OK when RCCL can be opened here (checked by every rank before the collective init, so
+ * that no rank enters ncclCommInitRank alone). */
+int zkl_comm_available(void);
+/* ncclGetUniqueId on the root rank; the 128 bytes go to the other ranks out of band
+ * (bench.py / zkl_hip.dist use the torch.distributed store). */
+int zkl_comm_unique_id(uint8_t id_out[128]);
+/* ncclCommInitRank on `device` (collective over the world). */
+int zkl_comm_init(int device, int world, int rank, const uint8_t id[128], zkl_comm** out);
+/* Collective: every rank contributes `len` host bytes; on `root`, *out (free with
+ * zkl_hip_free) receives the world blobs concatenated in rank order and lens_out[world] their
+ * lengths (other ranks may pass NULL).  Lengths are all-gathered first, then each rank's blob
+ * is sent to the root (grouped ncclSend / ncclRecv on the comm's stream). */
+int zkl_comm_gather_bytes(zkl_comm* comm, const uint8_t* data, size_t len, int root, uint8_t** out,
+                          size_t* lens_out);
+/* Device time (ms, HIP events on the comm stream) of the last gather: length exchange + sends. */
+double zkl_comm_last_ms(const zkl_comm* comm);
+void zkl_comm_destroy(zkl_comm* comm);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,6 +50,7 @@ def _step_worker(rank, world, port, q):
     import zkl_hip
     from zkl_hip import dist
     dist.init()
+    comm, cerr = dist.init_rccl(0)  # no GPU here: every rank gets the same error, gloo carries the bytes
     t, opi, w = oracle_lib.synth_segment(0x5EED7000 + rank, 5)
     inner = oracle_lib.prove(t, w, 32, opi, oracle_lib.default_options(w, 32, queries=4, grind=0))
     pi = zkl_hip.AirPublicInputs()
@@ -60,13 +61,13 @@ def _step_worker(rank, world, port, q):
     info.state_in_hash[:] = bytes([rank]) * 32       # chained: out(r) = in(r+1)
     info.state_out_hash[:] = bytes([rank + 1]) * 32
     step = zkl_hip.step_proof_encode(pi, info, inner)
-    steps = dist.collect_step_proofs([step])
+    steps = dist.collect_step_proofs([step], comm)
     root = None
     if steps is not None:
         root = zkl_hip.children_root(bytes(pi.program_id), [d["digest"] for d in steps],
                                      [d["root_trace"] for d in steps])
     q.put((rank, None if steps is None else [(d["segment_index"], d["digest"], d["root_trace"]) for d in steps],
-           zkl_hip.step_proof_digest(step), root, bytes(pi.program_id)))
+           zkl_hip.step_proof_digest(step), root, bytes(pi.program_id), (comm is None, cerr)))
     dist.shutdown()
 
 
@@ -84,13 +85,16 @@ def test_gloo_step_handoff_world_size_2():
     procs = [ctx.Process(target=_step_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = {}
+    res, transport = {}, {}
     for _ in range(2):
-        r, steps, own, root, suite = q.get(timeout=180)
+        r, steps, own, root, suite, tr = q.get(timeout=180)
         res[r] = (steps, own, root, suite)
+        transport[r] = tr
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    # RCCL could not start (no GPU): both ranks fell back together, with the reason
+    assert transport[0] == transport[1] and transport[0][0] and transport[0][1]
     steps, _, root, suite = res[0]
     assert res[1][0] is None and res[1][2] is None
     assert [s[0] for s in steps] == [0, 1]
@@ -191,3 +195,13 @@ def test_bench_launcher_propagates_rank_failure():
     r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], {"ZKL_BENCH_DEVICE": "99"})
     assert r.returncode != 0
     assert r.stdout.strip() == ""
+
+
+def test_step_blob_packing():
+    """One rank's step proofs travel as one RCCL payload: [u32 count][u64 len]*[bytes]."""
+    sys.path.insert(0, os.path.join(ROOT, "zk-lisp_amd"))
+    from zkl_hip import dist
+    for blobs in ([], [b""], [b"a"], [bytes(range(256)) * 3, b"", b"xyz"]):
+        assert dist.unpack_blobs(dist.pack_blobs(blobs)) == blobs
+    with pytest.raises(ValueError):
+        dist.unpack_blobs(dist.pack_blobs([b"abc"]) + b"!")

@@ -169,6 +169,14 @@ def load_library():
     lib.zkl_agg_trace.argtypes = [P(C.c_char_p), P(C.c_size_t), C.c_uint32, C.c_void_p, C.c_uint32, P(C.c_uint32)]
     lib.zkl_agg_trace_mode.argtypes = [P(C.c_char_p), P(C.c_size_t), C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32,
                                        P(C.c_uint32)]
+    lib.zkl_comm_unique_id.argtypes = [C.c_void_p]
+    lib.zkl_comm_available.argtypes = []
+    lib.zkl_comm_init.argtypes = [C.c_int, C.c_int, C.c_int, C.c_char_p, P(C.c_void_p)]
+    lib.zkl_comm_gather_bytes.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.c_int, P(P(C.c_uint8)),
+                                          P(C.c_size_t)]
+    lib.zkl_comm_last_ms.argtypes = [C.c_void_p]
+    lib.zkl_comm_last_ms.restype = C.c_double
+    lib.zkl_comm_destroy.argtypes = [C.c_void_p]
     _lib = lib
     return lib
 
@@ -478,6 +486,60 @@ def synth_vm_segment(seed: int, log_n: int, flags: int = 0):
     if rc != 0:
         raise ZklError(rc, "synth_vm_segment failed")
     return trace, pi, w.value
+
+
+def comm_available():
+    """None when RCCL can be opened in this process, else the reason."""
+    lib = load_library()
+    return None if lib.zkl_comm_available() == 0 else lib.zkl_hip_last_error(None).decode(errors="replace")
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId (zkl_comm_unique_id): 128 bytes the root hands to the other ranks."""
+    lib = load_library()
+    buf = (C.c_uint8 * 128)()
+    rc = lib.zkl_comm_unique_id(buf)
+    if rc:
+        raise ZklError(rc, lib.zkl_hip_last_error(None).decode(errors="replace"))
+    return bytes(buf)
+
+
+class Comm:
+    """RCCL communicator of one rank (zkl_comm_*): the multi-GPU boundary exchange of step
+    proofs to the aggregating rank."""
+
+    def __init__(self, device: int, world: int, rank: int, uid: bytes):
+        self.lib = load_library()
+        self.ptr = C.c_void_p()
+        self.world, self.rank = world, rank
+        rc = self.lib.zkl_comm_init(device, world, rank, bytes(uid), C.byref(self.ptr))
+        if rc:
+            raise ZklError(rc, self.lib.zkl_hip_last_error(None).decode(errors="replace"))
+
+    def gather_bytes(self, data: bytes, root: int = 0):
+        """Collective: list of every rank's bytes (rank order) on root, None elsewhere."""
+        out = C.POINTER(C.c_uint8)()
+        lens = (C.c_size_t * self.world)()
+        rc = self.lib.zkl_comm_gather_bytes(self.ptr, bytes(data), len(data), root, C.byref(out), lens)
+        if rc:
+            raise ZklError(rc, self.lib.zkl_hip_last_error(None).decode(errors="replace"))
+        if self.rank != root:
+            return None
+        blob = C.string_at(out, sum(lens)) if sum(lens) else b""
+        self.lib.zkl_hip_free(out)
+        res, off = [], 0
+        for n in lens:
+            res.append(blob[off:off + n])
+            off += n
+        return res
+
+    def last_ms(self) -> float:
+        return float(self.lib.zkl_comm_last_ms(self.ptr))
+
+    def close(self):
+        if self.ptr:
+            self.lib.zkl_comm_destroy(self.ptr)
+            self.ptr = C.c_void_p()
 
 
 class Context:

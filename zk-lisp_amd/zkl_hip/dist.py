@@ -1,14 +1,18 @@
 """Multi-GPU coordination for segment proving.
 
 Segments are independent, so ranks (one process per GPU, launched by
-torch.distributed.run) prove disjoint segment sets with no data-path collective.  The
-only communication is control: a barrier around the timed region, the max-over-ranks
-elapsed time, and (for the aggregation hand-off) gathering step-proof bytes on rank 0.
-It runs on torch.distributed's gloo backend with CPU tensors: the prover owns the GPU
-through its own HIP runtime (runtime note)."""
+torch.distributed.run) prove disjoint segment sets with no data-path collective.  The one
+exchange is the aggregation hand-off: the step proofs (and the boundary fields inside them)
+go to rank 0 over RCCL point-to-point transfers between the GPUs (zkl_comm_*, xGMI within a
+node).  Control -- the barrier around the timed region, the max-over-ranks elapsed time, the
+RCCL unique id -- runs on torch.distributed's gloo backend with CPU tensors: the prover owns
+the GPU through its own HIP runtime (runtime note)."""
 import os
+import struct
 
 _dist = None
+_comm = None
+_comm_error = None
 
 
 def env():
@@ -76,16 +80,86 @@ def gather_to_root(obj):
     return out
 
 
-def collect_step_proofs(step_bytes):
+def init_rccl(device):
+    """The RCCL communicator of this rank (zkl_hip.Comm): rank 0 draws the unique id and the
+    gloo control plane broadcasts it.  Returns (comm or None, error or None); a failure is
+    reported, and collect_step_proofs then uses the gloo path."""
+    global _comm, _comm_error
+    if _comm is not None or _comm_error is not None:
+        return _comm, _comm_error
+    import zkl_hip
+    rank, world, _ = env()
+    err, uid = None, None
+    if os.environ.get("ZKL_COMM", "rccl") == "gloo":
+        err = "ZKL_COMM=gloo"
+    # every rank must be able to enter ncclCommInitRank, or none does (it is collective)
+    avail = gather_to_root(err or zkl_hip.comm_available())
+    if rank == 0:
+        err = next((e for e in avail if e), None)
+        if err is None:
+            try:
+                uid = zkl_hip.comm_unique_id()
+            except Exception as e:  # noqa: BLE001  (reported in the bench line)
+                err = str(e)
+    box = [uid, err]
+    if _dist is not None:
+        _dist.broadcast_object_list(box, src=0)
+    uid, err = box
+    comm = None
+    if err is None:
+        try:
+            comm = zkl_hip.Comm(device, world, rank, uid)
+        except Exception as e:  # noqa: BLE001
+            err = str(e)
+    errs = gather_to_root(err) if _dist is not None else [err]
+    if _dist is not None:  # every rank takes the same transport
+        flag = [next((e for e in (errs or []) if e), None)] if rank == 0 else [None]
+        _dist.broadcast_object_list(flag, src=0)
+        err = flag[0]
+    if err is not None and comm is not None:
+        comm.close()
+        comm = None
+    _comm, _comm_error = comm, err
+    return comm, err
+
+
+def pack_blobs(blobs):
+    """[u32 count][u64 len]*count[bytes...]: one rank's step proofs as one RCCL payload."""
+    head = struct.pack("<I", len(blobs)) + b"".join(struct.pack("<Q", len(b)) for b in blobs)
+    return head + b"".join(bytes(b) for b in blobs)
+
+
+def unpack_blobs(buf):
+    (k,) = struct.unpack_from("<I", buf, 0)
+    lens = struct.unpack_from(f"<{k}Q", buf, 4)
+    out, off = [], 4 + 8 * k
+    for n in lens:
+        out.append(bytes(buf[off:off + n]))
+        off += n
+    if off != len(buf):
+        raise ValueError("malformed step-proof payload")
+    return out
+
+
+def gather_step_bytes(step_bytes, comm=None):
+    """Every rank's step encodings on rank 0 (list per rank), None elsewhere: over RCCL when a
+    communicator is given, else over gloo (host bytes)."""
+    if comm is not None:
+        got = comm.gather_bytes(pack_blobs(step_bytes), root=0)
+        return None if got is None else [unpack_blobs(b) for b in got]
+    return gather_to_root(list(step_bytes))
+
+
+def collect_step_proofs(step_bytes, comm=None):
     """Aggregation hand-off: every rank contributes the ZKLSTP1 encodings of
     the step proofs it produced; rank 0 receives all of them, decodes each one
     (StepProof::from_bytes field order, proof/step.rs:153-493), orders them by segment
     index and checks the boundary chain the aggregation AIR consumes (state_out_hash of
     segment i == state_in_hash of segment i+1) and the step digests (digest.rs:16-68).
-    Returns the ordered list of dicts on rank 0, None elsewhere.  The payload is a few
-    hundred KB per segment, so it travels over the gloo control plane as host bytes."""
+    Returns the ordered list of dicts on rank 0, None elsewhere.  The payload (~0.47 MB per
+    2^16-row segment) moves over RCCL when `comm` is given (gather_step_bytes)."""
     from . import parse_step_proof, step_proof_digest
-    got = gather_to_root(list(step_bytes))
+    got = gather_step_bytes(step_bytes, comm)
     if got is None:
         return None
     steps = []
@@ -108,7 +182,10 @@ def collect_step_proofs(step_bytes):
 
 
 def shutdown():
-    global _dist
+    global _dist, _comm, _comm_error
+    if _comm is not None:
+        _comm.close()
+    _comm, _comm_error = None, None
     if _dist is not None:
         _dist.destroy_process_group()
         _dist = None
