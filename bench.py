@@ -46,6 +46,7 @@ SEED0 = 0x5EED0001             # segment seed of rank / segment 0 (SURVEY §8(d)
 GOLDEN = os.path.join(ROOT, "tests", "golden", "proof_2p16.json")
 CHAIN = os.path.join(ROOT, "tests", "golden", "chain_2p16.json")  # the multi-segment program (make_chain_goldens.py)
 VALU_MIX = os.path.join(ROOT, "profiles", "r02", "valu_mix.json")
+VALU_FLOOR = os.path.join(ROOT, "profiles", "r03", "valu_floor.json")
 ROW_KERNEL = {"mfma": "hash_rows_pm_kernel<0>", "lane": "hash_rows_kernel<0>"}
 
 
@@ -229,7 +230,17 @@ def valu_roofline(perms_per_s):
     except (OSError, ValueError):
         return None
     peak = mix["peak_perms_per_s"]
-    return {"bound": "valu-issue (instruction-mix ceiling)", "kernel": mix["kernel"],
+    try:
+        floor = json.load(open(VALU_FLOOR))
+    except (OSError, ValueError):
+        floor = None
+    extra = {}
+    if floor:
+        extra = {"algorithm_floor_perms_per_s_M": round(floor["floor_perms_per_s"] / 1e6, 1),
+                 "frac_of_algorithm_floor": round(perms_per_s / floor["floor_perms_per_s"], 4),
+                 "algorithm_valu_per_element_round": floor["valu_per_element_round"],
+                 "kernel_valu_per_element_round": floor["kernel_valu_per_element_round"]}
+    return {"bound": "valu-issue (instruction-mix ceiling)", "kernel": mix["kernel"], **extra,
             "achieved": round(perms_per_s / 1e6, 1), "peak": round(peak / 1e6, 1), "unit": "M permutations/s",
             "frac": round(perms_per_s / peak, 4),
             "valu_per_perm_round_loop": mix["valu_per_perm_round_loop"],

@@ -526,6 +526,11 @@ static inline unsigned pg_blocks(size_t items) {
   return (unsigned)((items + per - 1) / per);
 }
 
+// PM_ROW_BIG_CFG: row hashing keeps the partition digests in LDS for every partition count
+// (the <TAG, true> form) instead of in registers (fewer VGPRs, for PM_ROW_WAVES_CFG = 12)
+#ifndef PM_ROW_BIG_CFG
+#define PM_ROW_BIG_CFG 0
+#endif
 #include "poseidon_mfma.inc"
 
 // ---- row hashing (Winterfell partitioned row hash): one group per row.  The row's
@@ -607,7 +612,7 @@ void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np
   // partitioned rows end in merge_many (rule 0: even of one digest)
   const uint32_t merge = row_digest_rule() == 0 ? (psize != ncols) : (np_eff > 1);
   if (hash_engine() == 1 && nrows >= pm_min_items() && np_eff <= (uint32_t)PM_MAX_PARTS) {
-    if (np_eff > 9)
+    if (np_eff > 9 || PM_ROW_BIG_CFG)
       PM_GO((hash_rows_pm_kernel<0, true>), nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out);
     else if (tag == 1)
       PM_GO((hash_rows_pm_kernel<1, false>), nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out);

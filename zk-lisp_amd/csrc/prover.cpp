@@ -748,7 +748,10 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   if (o.grinding_factor == 0) {
     nonce = 1;
   } else {
-    uint32_t batch = 1u << 16;
+    // ascending windows of nonces, the minimum of the first window that holds a solution; the
+    // first window is 2^(g+1) tries (a solution with probability 1 - e^-2 = 0.86), so one
+    // launch and one read-back usually settle it
+    uint32_t batch = 1u << std::min<uint32_t>(std::max<uint32_t>(o.grinding_factor + 1, 14), 22);
     for (uint64_t base = 1; nonce == 0; base += batch, batch = std::min<uint32_t>(batch * 2, 1u << 22)) {
       unsigned long long init = ~0ull;
       HIPCHECK(hipMemcpyAsync(C->best.p, &init, 8, hipMemcpyHostToDevice, s));
