@@ -214,8 +214,10 @@ int zkl_hip_set_hash_policy(int engine, uint32_t pm_min_items);
 int zkl_hip_set_row_digest_rule(int rule);
 int zkl_hip_row_digest_rule(void);
 /* Process-wide NTT form for evaluation (DIT) passes: 1 (default) lazily reduced 26-bit limbs
- * inside a pass, 0 the canonical-form kernel.  Identical results; for parity tests / A-B. */
-int zkl_hip_set_ntt_mode(int lazy);
+ * inside a pass, 0 the canonical-form kernel, 2 the lazy form with its 8-stage passes on the
+ * matrix cores (slower on gfx950).  Identical results; for parity tests /
+ * A-B. */
+int zkl_hip_set_ntt_mode(int mode);
 /* Coset low-degree extension of column-major n_cols x n_rows evaluations over
  * GENERATOR * <w_{n*blowup}>; writes coefficients (n_cols x n_rows) and the LDE
  * (n_cols x n_rows*blowup), both column-major, natural order. */

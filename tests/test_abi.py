@@ -132,3 +132,16 @@ def test_row_digest_rule_switch():
         assert lib.zkl_hip_row_digest_rule() == 1
     assert lib.zkl_hip_row_digest_rule() == 0
     assert lib.zkl_hip_set_row_digest_rule(2) == -1
+
+
+def test_ntt_mode_switch_bounds():
+    """zkl_hip_set_ntt_mode: 0 canonical, 1 lazy (default), 2 lazy + matrix-core passes."""
+    import zkl_hip
+    lib = zkl_hip.load_library()
+    try:
+        for mode in (0, 2, 1):
+            assert lib.zkl_hip_set_ntt_mode(mode) == 0
+        assert lib.zkl_hip_set_ntt_mode(3) == -1
+        assert lib.zkl_hip_set_ntt_mode(-1) == -1
+    finally:
+        lib.zkl_hip_set_ntt_mode(1)

@@ -507,7 +507,7 @@ def test_lde_lazy_ntt_matches_canonical(gpu_ctx, ncols, log_n, blow):
     gpu_ctx.upload(d_v, raw, len(raw))
     outs = []
     try:
-        for lazy in (0, 1):
+        for lazy in (0, 1, 2):
             assert lib.zkl_hip_set_ntt_mode(lazy) == 0
             gpu_ctx.lde(d_v, ncols, n, blow, d_c, d_l)
             outs.append(gpu_ctx.download(d_l, 16 * ncols * N))
@@ -515,7 +515,7 @@ def test_lde_lazy_ntt_matches_canonical(gpu_ctx, ncols, log_n, blow):
         lib.zkl_hip_set_ntt_mode(1)
         for d in (d_v, d_c, d_l):
             gpu_ctx.free(d)
-    assert outs[0] == outs[1]
+    assert outs[0] == outs[1] == outs[2]
 
 
 def test_full_size_proof_independent_of_kernel_forms(gpu_ctx):
@@ -530,7 +530,8 @@ def test_full_size_proof_independent_of_kernel_forms(gpu_ctx):
     proofs = {}
     try:
         for name, engine, min_items, lazy in (("default", 1, 1 << 14, 1), ("lane", 0, 1 << 14, 1),
-                                              ("all_mfma", 1, 32, 1), ("canonical_ntt", 1, 1 << 14, 0)):
+                                              ("all_mfma", 1, 32, 1), ("canonical_ntt", 1, 1 << 14, 0),
+                                              ("mfma_ntt", 1, 1 << 14, 2)):
             assert lib.zkl_hip_set_hash_policy(engine, min_items) == 0
             assert lib.zkl_hip_set_ntt_mode(lazy) == 0
             proofs[name] = gpu_ctx.prove_segment(t, w, n, pi, opts)

@@ -11,7 +11,9 @@
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <set>
 #include <stdexcept>
 #include <vector>
 
@@ -1176,6 +1178,8 @@ __global__ __launch_bounds__(NTT8_THREADS) __global__ __launch_bounds__(NTT8_THR
   }
 }
 
+#include "ntt_mfma.inc"
+
 // DIT form: lazy limbs (default) or the canonical kernel (ZKL_NTT=classic, set_ntt_lazy)
 static std::atomic<int> g_ntt_lazy{-1};
 static bool ntt_lazy_enabled() {
@@ -1284,6 +1288,10 @@ static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
         const size_t Gw = wide ? 2 * G : G;
         const unsigned grid = (unsigned)((groups + Gw - 1) / Gw);
         const fe* sp = cur == lo ? src : nullptr;
+        if (r == 8 && launch_ntt_dit8_mfma(d, ncols, logN, cur, sp, src_logb, s)) {
+          cur += r;
+          continue;
+        }
         if (r == 8 && ntt8_enabled() && ((size_t)1 << cur) >= (size_t)NTT8_G && (N >> 8) >= (size_t)NTT8_G)
           ntt_dit8_kernel<<<(unsigned)(groups / NTT8_G), NTT8_THREADS, 0, s>>>(d, ncols, logN, cur, roots, sp, src_logb,
                                                                               ntt8_lfast(cur));

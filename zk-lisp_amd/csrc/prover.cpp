@@ -1135,9 +1135,10 @@ int zkl_hip_hash_rows(zkl_ctx* c, const void* d_m, uint32_t nc, uint32_t nr, uin
   });
 }
 
-int zkl_hip_set_ntt_mode(int lazy) {
-  if (lazy < 0 || lazy > 1) return ZKL_E_INVALID;
-  set_ntt_lazy(lazy != 0);
+int zkl_hip_set_ntt_mode(int mode) {
+  if (mode < 0 || mode > 2) return ZKL_E_INVALID;
+  set_ntt_lazy(mode != 0);
+  set_ntt_mfma(mode == 2);
   return 0;
 }
 
