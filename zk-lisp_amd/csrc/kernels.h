@@ -71,8 +71,10 @@ void upload_deep_coeffs(ProofConsts* dK, const fe* h_coeffs, int n, hipStream_t 
 // Row digests of a column-major matrix (ld = rows per column) with Winterfell partitioning.
 // d_tmp: scratch of n_parts * n_rows elements (unused when a single hash covers the row).
 // tag: 0 = trace commitment, 1 = composition commitment (distinct kernel symbols in profiles)
+// split: d_mat is a trace LDE in the split layout; the kernels walk positions q (whole lines)
+// and write each digest to its row lde_row(q).
 void launch_hash_rows(const fe* d_mat, uint32_t n_cols, size_t n_rows, uint32_t num_partitions,
-                      uint32_t hash_rate, fe* d_tmp, fe* d_out, hipStream_t s, int tag = 0);
+                      uint32_t hash_rate, fe* d_tmp, fe* d_out, hipStream_t s, int tag = 0, int split = 0);
 // Merkle tree: d_nodes[n..2n) must hold the leaves; fills d_nodes[1..n).
 void launch_merkle(fe* d_nodes, size_t n_leaves, hipStream_t s);
 // out[i] = merge_with_int(seed, base + 1 + i)   (RandomCoin::draw, counter base+1+i)
@@ -103,8 +105,32 @@ void launch_ntt_stages(fe* d_data, size_t n_cols, size_t N, bool dif, int lo_log
 // by the coset shift (c_k * 3^k at position bitrev(k)); d_out (N per column, natural order)
 // = evaluations over 3*<w_N>.  The first DIT pass reads the blowup copies straight from
 // d_coef.
-void launch_lde_from_coeffs(const fe* d_coef, size_t n_cols, size_t n, size_t N, MontTab roots, size_t Ntab, fe* d_out,
-                            hipStream_t s);
+// want_split: store the evaluations in the split layout (lde_pos below) when the last pass
+// supports it; returns 1 when the output is split, 0 when it is in natural order.
+int launch_lde_from_coeffs(const fe* d_coef, size_t n_cols, size_t n, size_t N, MontTab roots, size_t Ntab, fe* d_out,
+                           hipStream_t s, bool want_split = false);
+// Even/odd split layout of a trace LDE column.  Write the N = 256 S rows as
+// r = L + t S (L < S, t < 256); the last DIT pass owns, per block, 8 consecutive L (L0 + l)
+// and all t, and must store in place, so the layout permutes within that set: row (L, t) goes
+// to L' = L0 + l / 2 + 4 (t & 1), t' = t / 2 + 128 (l & 1).  Every even row thus sits in the
+// first half of its column (the constraint evaluator reads only those, in whole 128-byte
+// lines) and every line holds eight rows of one parity.  Needs S >= 8.
+__host__ __device__ inline size_t lde_pos(size_t r, size_t N, int split) {
+  if (!split) return r;
+  const int logS = __builtin_ctzll((unsigned long long)N) - 8;
+  const size_t S = (size_t)1 << logS;
+  const size_t L = r & (S - 1), t = r >> logS, l = L & 7;
+  return (L - l) + (l >> 1) + ((t & 1) << 2) + (((t >> 1) + ((l & 1) << 7)) << logS);
+}
+// inverse of lde_pos: the row stored at position q
+__host__ __device__ inline size_t lde_row(size_t q, size_t N, int split) {
+  if (!split) return q;
+  const int logS = __builtin_ctzll((unsigned long long)N) - 8;
+  const size_t S = (size_t)1 << logS;
+  const size_t Lp = q & (S - 1), tp = q >> logS, m = Lp & 7;
+  const size_t l = ((m & 3) << 1) | (tp >> 7), t = ((tp & 127) << 1) | (m >> 2);
+  return (Lp - m) + l + (t << logS);
+}
 // out[c*N + B*j + t] = in[c*stride + off + src(j)*estride] * scale[bitrev_n(j)] * mult for t < B (B = N/n);
 // src(j) = j or n-1-j
 void launch_broadcast(const fe* d_in, size_t in_col_stride, size_t in_elem_stride, size_t in_offset,
@@ -137,7 +163,7 @@ void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, con
                             const fe* d_bm /* (n_bcols + 1) x ce */, const CeParams& p, ProofConsts* dK,
                             bool pose_block, bool ram_merkle,
                             fe* d_xinv /* ce entries: 1 / (x_i - g^(n-1)) */, bool xinv_ready, fe* d_out,
-                            hipStream_t s);
+                            hipStream_t s, int split = 0);
 // boundary vectors: vec[slot*n + step] = beta_a ; wv[s] = sum beta_a*value_a over assertions at step s
 void launch_boundary_scatter(const uint32_t* d_slot, const uint32_t* d_step, const fe* d_beta, size_t n_assert,
                              size_t n, fe* d_vecs, hipStream_t s);
@@ -166,7 +192,8 @@ struct DeepParams {
 // d_dinv[i] = 1/((x_i - z)(x_i - zg)) over the LDE coset x_i = 3*w_N^i (launch before launch_deep)
 void launch_deep_denoms(const fe* d_roots, size_t Ntab, size_t N, fe z, fe zg, fe* d_dinv, hipStream_t s);
 void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p,
-                 const ProofConsts* dK, const fe* d_dinv /* from launch_deep_denoms */, fe* d_out, hipStream_t s);
+                 const ProofConsts* dK, const fe* d_dinv /* from launch_deep_denoms */, fe* d_out, hipStream_t s,
+                 int split = 0);
 void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s);
 // alpha read from device memory (written by launch_fri_coin)
 void launch_fri_fold(const fe* d_ev, size_t Nd, const fe* d_alpha, const fe* d_iroots, size_t Ntab, fe* d_out,

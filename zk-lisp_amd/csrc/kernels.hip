@@ -541,7 +541,7 @@ static inline unsigned pg_blocks(size_t items) {
 // TAG only separates the trace (0) and composition (1) commitments in profiles
 template <int TAG>
 __global__ PG_KERNEL void hash_rows_kernel(const fe* __restrict__ M, uint32_t ncols, size_t nrows,
-                                                        uint32_t psize, uint32_t merge, fe* __restrict__ out) {
+                                                        uint32_t psize, uint32_t merge, fe* __restrict__ out, int split) {
   PG_SETUP();
   const bool live = P.g < PG_PER_WAVE && item < nrows;
   const size_t row = live ? item : 0;
@@ -550,7 +550,7 @@ __global__ PG_KERNEL void hash_rows_kernel(const fe* __restrict__ M, uint32_t nc
   for (uint32_t p = 0; p < np; p++) {
     const uint32_t c0 = p * psize;
     const uint32_t len = min(psize, ncols - c0);
-    const fe* base = M + (size_t)c0 * nrows + row;
+    const fe* base = M + (size_t)c0 * nrows + row;  // position (split: the row is lde_row)
     d = pg_sponge<DOM_ELEMS>(P, live, (int)((len + 1) / 2), [&](int j) {
       fe a = base[(size_t)(2 * j) * nrows];
       fe b = (2u * j + 1 < len) ? base[(size_t)(2 * j + 1) * nrows] : fe_zero();
@@ -564,7 +564,7 @@ __global__ PG_KERNEL void hash_rows_kernel(const fe* __restrict__ M, uint32_t nc
     }
   }
   if (merge) d = pg_sponge<DOM_MANY>(P, live, (int)np, [&](int i) { return i + 1 < 10 ? keep0 : keep1; });
-  if (live && P.j == 0) out[row] = d;
+  if (live && P.j == 0) out[lde_row(row, nrows, split)] = d;
 }
 
 __global__ PG_KERNEL void merkle_level_kernel(fe* nodes, size_t lvl) {
@@ -603,7 +603,7 @@ void set_row_digest_rule(int r) { g_row_rule.store(r ? 1 : 0); }
 int row_digest_rule() { return g_row_rule.load(); }
 
 void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np, uint32_t rate, fe* d_tmp, fe* d_out,
-                      hipStream_t s, int tag) {
+                      hipStream_t s, int tag, int split) {
   (void)d_tmp;
   uint32_t psize = ncols;
   if (np > 1) {
@@ -615,17 +615,17 @@ void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np
   const uint32_t merge = row_digest_rule() == 0 ? (psize != ncols) : (np_eff > 1);
   if (hash_engine() == 1 && nrows >= pm_min_items() && np_eff <= (uint32_t)PM_MAX_PARTS) {
     if (np_eff > 9 || PM_ROW_BIG_CFG)
-      PM_GO((hash_rows_pm_kernel<0, true>), nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out);
+      PM_GO((hash_rows_pm_kernel<0, true>), nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out, split);
     else if (tag == 1)
-      PM_GO((hash_rows_pm_kernel<1, false>), nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out);
+      PM_GO((hash_rows_pm_kernel<1, false>), nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out, split);
     else
-      PM_GO((hash_rows_pm_kernel<0, false>), nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out);
+      PM_GO((hash_rows_pm_kernel<0, false>), nrows, true, s)(d_mat, ncols, nrows, psize, merge, d_out, split);
     return;
   }
   if (tag == 1)
-    hash_rows_kernel<1><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, merge, d_out);
+    hash_rows_kernel<1><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, merge, d_out, split);
   else
-    hash_rows_kernel<0><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, merge, d_out);
+    hash_rows_kernel<0><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, merge, d_out, split);
 }
 
 __global__ __launch_bounds__(256) void merkle_level_wide_kernel(fe* nodes, size_t lvl) {
@@ -1071,7 +1071,7 @@ constexpr int NTT8_THREADS = 256;
 constexpr int NTT8_PITCH = 257;
 __global__ __launch_bounds__(NTT8_THREADS) __global__ __launch_bounds__(NTT8_THREADS) void ntt_dit8_kernel(fe* __restrict__ data, size_t ncols, int logN, int logS,
                                                                  MontTab roots, const fe* __restrict__ src, int src_logb,
-                                                                 int lfast) {
+                                                                 int lfast, int split) {
   __shared__ uint4 bufA[NTT8_G * NTT8_PITCH];
   __shared__ uint32_t bufB[NTT8_G * NTT8_PITCH];
   const int tid = (int)threadIdx.x;
@@ -1173,8 +1173,14 @@ __global__ __launch_bounds__(NTT8_THREADS) __global__ __launch_bounds__(NTT8_THR
     bfly(y2, y3, w[3 * qd]);
     bfly(y0, y2, w[3 * qd + 1]);
     bfly(y1, y3, w[3 * qd + 2]);
+    // split (last pass only, S = N / 256, so L & 7 = g): row L + t S with t = a2 + 64 u goes to
+    // lde_pos = (L - g) + g / 2 + 4 (t & 1) + (t / 2 + 128 (g & 1)) S, i.e. 32 S apart in u
+    const size_t at0 = split ? (col << logN) + (L - g) + (g >> 1) + 4 * (a2 & 1) +
+                                   ((size_t)((a2 >> 1) + ((g & 1) << 7)) << logS)
+                             : base + (size_t)a2 * S;
+    const size_t du = split ? 32 * S : 64 * S;
 #pragma unroll
-    for (int u = 0; u < 4; u++) data[base + (size_t)(a2 + 64 * u) * S] = ntt_canon(x[4 * qd + u]);
+    for (int u = 0; u < 4; u++) data[at0 + u * du] = ntt_canon(x[4 * qd + u]);
   }
 }
 
@@ -1259,8 +1265,18 @@ static std::vector<int> ntt_split(int K) {
   return rs;
 }
 
+// DIT passes over stages [lo, hi]: can the last one store the split layout (it must be the
+// 8-stage register pass, whose store is the only one that knows the layout)?
+static bool dit_split_ok(size_t N, int lo, int hi) {
+  if (hi < lo || !ntt_lazy_enabled() || !ntt8_enabled() || ntt_mfma_enabled()) return false;
+  const std::vector<int> rs = ntt_split(hi - lo + 1);
+  int cur = lo;
+  for (size_t k = 0; k + 1 < rs.size(); k++) cur += rs[k];
+  return rs.back() == 8 && ((size_t)1 << cur) >= (size_t)NTT8_G && (N >> 8) >= (size_t)NTT8_G;
+}
+
 static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, MontTab roots, size_t Ntab,
-                       const fe* src, int src_logb, hipStream_t s) {
+                       const fe* src, int src_logb, hipStream_t s, int split = 0) {
   int logN = ilog2s(N), logTab = ilog2s(Ntab);
   if (hi < lo) return;
   const std::vector<int> rs = ntt_split(hi - lo + 1);
@@ -1277,7 +1293,9 @@ static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
     }
   } else {
     int cur = lo;
-    for (const int r : rs) {
+    for (size_t ri = 0; ri < rs.size(); ri++) {
+      const int r = rs[ri];
+      const int split_here = split && ri + 1 == rs.size();
       size_t groups = (N >> r) * ncols;
       size_t G = NTT_ELEMS >> r;
       if (ntt_lazy_enabled()) {
@@ -1288,13 +1306,13 @@ static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
         const size_t Gw = wide ? 2 * G : G;
         const unsigned grid = (unsigned)((groups + Gw - 1) / Gw);
         const fe* sp = cur == lo ? src : nullptr;
-        if (r == 8 && launch_ntt_dit8_mfma(d, ncols, logN, cur, sp, src_logb, s)) {
+        if (!split_here && r == 8 && launch_ntt_dit8_mfma(d, ncols, logN, cur, sp, src_logb, s)) {
           cur += r;
           continue;
         }
         if (r == 8 && ntt8_enabled() && ((size_t)1 << cur) >= (size_t)NTT8_G && (N >> 8) >= (size_t)NTT8_G)
           ntt_dit8_kernel<<<(unsigned)(groups / NTT8_G), NTT8_THREADS, 0, s>>>(d, ncols, logN, cur, roots, sp, src_logb,
-                                                                              ntt8_lfast(cur));
+                                                                              ntt8_lfast(cur), split_here);
         else if (wide && wm == 2)
           ntt_dit_lazy_kernel<2 * NTT_ELEMS, 2 * NTT_THREADS><<<grid, 2 * NTT_THREADS, 0, s>>>(d, ncols, logN, r, cur, roots, sp, src_logb);
         else if (wide)
@@ -1314,15 +1332,17 @@ void launch_ntt_stages(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
   ntt_passes(d, ncols, N, dif, lo, hi, roots, Ntab, nullptr, 0, s);
 }
 
-void launch_lde_from_coeffs(const fe* d_coef, size_t ncols, size_t n, size_t N, MontTab roots, size_t Ntab, fe* d_out,
-                            hipStream_t s) {
+int launch_lde_from_coeffs(const fe* d_coef, size_t ncols, size_t n, size_t N, MontTab roots, size_t Ntab, fe* d_out,
+                           hipStream_t s, bool want_split) {
   const int logB = ilog2s(N / n);
   if (logB == 0) {
     ZKL_HIPCHECK(hipMemcpyAsync(d_out, d_coef, ncols * n * sizeof(fe), hipMemcpyDeviceToDevice, s));
     ntt_passes(d_out, ncols, N, false, 0, ilog2s(N) - 1, roots, Ntab, nullptr, 0, s);
-    return;
+    return 0;
   }
-  ntt_passes(d_out, ncols, N, false, logB, ilog2s(N) - 1, roots, Ntab, d_coef, logB, s);
+  const int split = want_split && dit_split_ok(N, logB, ilog2s(N) - 1) ? 1 : 0;
+  ntt_passes(d_out, ncols, N, false, logB, ilog2s(N) - 1, roots, Ntab, d_coef, logB, s, split);
+  return split;
 }
 
 __global__ void broadcast_kernel(const fe* __restrict__ in, size_t in_col_stride, size_t in_elem_stride,
@@ -1370,14 +1390,21 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
                                                               int roots_shift, const fe* __restrict__ pertab,
                                                               const fe* __restrict__ bm,
                                                               const ProofConsts* __restrict__ K,
-                                                              const fe* __restrict__ xinv, fe* __restrict__ out) {
+                                                              const fe* __restrict__ xinv, fe* __restrict__ out,
+                                                              int split) {
   const AirDevice& c_air = K->air;
   const CeParams& c_ce = K->ce;
   const size_t ce = c_ce.ce, N = c_ce.N;
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ce) return;
-  const size_t r0 = i * (N / ce);
-  const size_t r1 = (r0 + c_ce.blowup) & (N - 1);
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= ce) return;
+  // split layout with N / ce <= 2 (the CE rows are the even rows, or all rows): thread k reads
+  // position k, i.e. whole lines of the first half of each column, and evaluates the CE point
+  // of the row stored there; a wave's CE indices form two runs of 32.  Otherwise thread k
+  // evaluates CE point k.
+  const bool by_pos = split && N <= 2 * ce;
+  const size_t i = by_pos ? lde_row(k, N, 1) / (N / ce) : k;
+  const size_t r0 = by_pos ? k : lde_pos(i * (N / ce), N, split);
+  const size_t r1 = lde_pos((i * (N / ce) + c_ce.blowup) & (N - 1), N, split);
   auto cur = [&](int c) { return lde[(size_t)c * N + r0]; };
   auto nxt = [&](int c) { return lde[(size_t)c * N + r1]; };
   fe x = fe_mul(fe{3, 0}, roots[i << roots_shift]);
@@ -1432,20 +1459,20 @@ static void launch_coset_inv(const fe* d_roots, int shift, size_t M, fe a1, fe a
 
 void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab, const fe* d_bm,
                             const CeParams& p, ProofConsts* dK, bool pose_block, bool ram_merkle, fe* d_xinv,
-                            bool xinv_ready, fe* d_out, hipStream_t s) {
+                            bool xinv_ready, fe* d_out, hipStream_t s, int split) {
   ZKL_HIPCHECK(hipMemcpyAsync(&dK->ce, &p, sizeof p, hipMemcpyHostToDevice, s));
   int shift = ilog2s(Ntab) - ilog2s(p.ce);
   // 1 / (x - g^(n-1)) over the CE coset depends on the shape only: the caller keeps it per context
   if (!xinv_ready) launch_coset_inv(d_roots, shift, p.ce, p.gl, fe_zero(), 0, d_xinv, s);
   const unsigned grid = (unsigned)((p.ce + 255) / 256);
   if (pose_block && ram_merkle)
-    constraint_eval_kernel<true, true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out);
+    constraint_eval_kernel<true, true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
   else if (pose_block)
-    constraint_eval_kernel<true, false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out);
+    constraint_eval_kernel<true, false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
   else if (ram_merkle)
-    constraint_eval_kernel<false, true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out);
+    constraint_eval_kernel<false, true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
   else
-    constraint_eval_kernel<false, false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out);
+    constraint_eval_kernel<false, false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
 }
 
 __global__ void boundary_scatter_kernel(const uint32_t* slot, const uint32_t* step, const fe* beta, size_t na, size_t n,
@@ -1537,7 +1564,7 @@ __device__ __forceinline__ fe limbs_canon(const uint32_t l[5]) {
 __global__ __launch_bounds__(256) void deep_kernel(const fe* __restrict__ lde, const fe* __restrict__ clde,
                                                    const fe* __restrict__ roots, int shift, DeepParams p,
                                                    const ProofConsts* __restrict__ K, const fe* __restrict__ dinv,
-                                                   fe* out) {
+                                                   fe* out, int split) {
   const size_t T = (size_t)gridDim.x * blockDim.x;
   const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t col[DEEP_PTS][10];
@@ -1551,9 +1578,13 @@ __global__ __launch_bounds__(256) void deep_kernel(const fe* __restrict__ lde, c
 #pragma unroll
     for (int cc = 0; cc < DEEP_COLS; cc++) {
       const uint32_t c = c0 + cc;
-      const fe* src = c < p.W ? lde + (size_t)c * p.N : clde + (size_t)(c - p.W) * p.N;
+      // thread point k is LDE position q = i0 + k T (whole lines of the trace columns, which may
+      // be in the split layout), i.e. row lde_row(q); composition columns are in natural order
+      const bool tr = c < p.W;
+      const fe* src = tr ? lde + (size_t)c * p.N : clde + (size_t)(c - p.W) * p.N;
 #pragma unroll
-      for (int k = 0; k < DEEP_PTS; k++) v[cc][k] = c < ncol ? src[i0 + k * T] : fe_zero();
+      for (int k = 0; k < DEEP_PTS; k++)
+        v[cc][k] = c < ncol ? src[tr ? i0 + k * T : lde_row(i0 + k * T, p.N, split)] : fe_zero();
     }
 #pragma unroll
     for (int cc = 0; cc < DEEP_COLS; cc++) {
@@ -1575,7 +1606,7 @@ __global__ __launch_bounds__(256) void deep_kernel(const fe* __restrict__ lde, c
     uint32_t l[5];
     redc(col[k], l);
     const fe sv = limbs_canon(l);
-    const size_t i = i0 + k * T;
+    const size_t i = lde_row(i0 + k * T, p.N, split);
     const fe x = fe_mul(fe{3, 0}, roots[i << shift]);
     const fe d1 = fe_sub(x, p.z), d2 = fe_sub(x, p.zg);
     const fe num = fe_add(fe_mul(fe_sub(sv, p.sz), d2), fe_mul(fe_sub(sv, p.szg), d1));
@@ -1587,11 +1618,11 @@ void launch_deep_denoms(const fe* d_roots, size_t Ntab, size_t N, fe z, fe zg, f
 }
 
 void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p,
-                 const ProofConsts* dK, const fe* d_dinv, fe* d_out, hipStream_t s) {
+                 const ProofConsts* dK, const fe* d_dinv, fe* d_out, hipStream_t s, int split) {
   // N is a power of two >= 64: every thread gets exactly DEEP_PTS points
   const size_t threads = std::min<size_t>(256, p.N / DEEP_PTS);
   deep_kernel<<<(unsigned)(p.N / (threads * DEEP_PTS)), (unsigned)threads, 0, s>>>(
-      d_lde, d_clde, d_roots, ilog2s(Ntab) - ilog2s(p.N), p, dK, d_dinv, d_out);
+      d_lde, d_clde, d_roots, ilog2s(Ntab) - ilog2s(p.N), p, dK, d_dinv, d_out, split);
 }
 
 // FRI layer leaves: hash_elements([e_i, e_{i+Nd/2}]) (FriProver::build_layer, folding 2)

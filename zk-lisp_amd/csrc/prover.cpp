@@ -249,6 +249,12 @@ struct StageTimer {
 
 // ZKL_HOST_TRACE=1: host timestamps (us since the call) of the phases around host round trips
 static const bool g_host_trace = getenv("ZKL_HOST_TRACE") != nullptr;
+// trace LDE in the even/odd split layout (kernels.h lde_pos): ZKL_LDE_SPLIT=0
+// keeps natural order (A/B)
+static const bool g_lde_split = [] {
+  const char* e = getenv("ZKL_LDE_SPLIT");
+  return !(e && !strcmp(e, "0"));
+}();
 #define HT(label)                                                                                   \
   do {                                                                                              \
     if (g_host_trace)                                                                               \
@@ -386,11 +392,13 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->coef.ensure((size_t)W * n * sizeof(fe));
   C->lde.ensure((size_t)W * N * sizeof(fe));
   // columns [c0, c0 + nc): iNTT -> n*coef bit-reversed, scale c_k * 3^k (coset shift), DIT
+  // every chunk takes the same pass split, so all columns share one layout
+  int split = 0;
   auto lde_cols = [&](uint32_t c0, uint32_t nc) {
     fe* cf = C->coef.f() + (size_t)c0 * n;
     launch_ntt_stages(cf, nc, n, true, 0, logn - 1, miroots, Ntab, s);
     launch_scale_bitrev(cf, nc, n, C->opow_n.f(), s);
-    launch_lde_from_coeffs(cf, nc, n, N, mroots, Ntab, C->lde.f() + (size_t)c0 * N, s);
+    split = launch_lde_from_coeffs(cf, nc, n, N, mroots, Ntab, C->lde.f() + (size_t)c0 * N, s, g_lde_split);
   };
   if (trace_on_host) {
     KScope k(C, KF_NTT);
@@ -408,7 +416,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->tree.ensure(2 * N * sizeof(fe));
   {
     KScope k(C, KF_TRACE_HASH);
-    launch_hash_rows(C->lde.f(), W, N, o.num_partitions, o.hash_rate, C->parts.f(), C->tree.f() + N, s);
+    launch_hash_rows(C->lde.f(), W, N, o.num_partitions, o.hash_rate, C->parts.f(), C->tree.f() + N, s, 0, split);
   }
   check_launch("trace row hash");
   {
@@ -545,7 +553,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
       C->cexinv.ensure(ce * sizeof(fe));
     }
     launch_constraint_eval(C->lde.f(), roots, Ntab, C->pertab.f(), C->bm.f(), cp, dK, air.dev.pose_block != 0,
-                           (air.dev.ram_block | air.dev.merkle_block) != 0, C->cexinv.f(), ready, C->ce.f(), s);
+                           (air.dev.ram_block | air.dev.merkle_block) != 0, C->cexinv.f(), ready, C->ce.f(), s, split);
     C->cexinv_key_n = n; C->cexinv_key_ce = ce; C->cexinv_key_tab = Ntab; C->cexinv_key_roots = roots;
   }
   check_launch("constraint evaluation");
@@ -671,7 +679,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->deep.ensure(N * sizeof(fe));
   {
     KScope k(C, KF_DEEP);
-    launch_deep(C->lde.f(), C->clde.f(), roots, Ntab, dp, dK, C->xinv.f(), C->deep.f(), s);
+    launch_deep(C->lde.f(), C->clde.f(), roots, Ntab, dp, dK, C->xinv.f(), C->deep.f(), s, split);
   }
   check_launch("DEEP composition");
   T.mark(6);
@@ -784,7 +792,8 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   // gather plan: trace rows, comp rows, trace/comp tree nodes, FRI values + tree nodes
   std::vector<uint64_t> addrs;
   auto A = [&](const fe* p) { addrs.push_back((uint64_t)(uintptr_t)p); };
-  for (size_t k = 0; k < nq; k++) for (uint32_t c = 0; c < W; c++) A(C->lde.f() + (size_t)c * N + pos[k]);
+  for (size_t k = 0; k < nq; k++)
+    for (uint32_t c = 0; c < W; c++) A(C->lde.f() + (size_t)c * N + lde_pos(pos[k], N, split));
   for (size_t k = 0; k < nq; k++) for (int j = 0; j < Cc; j++) A(C->clde.f() + (size_t)j * N + pos[k]);
   auto tplan = batch_plan(N, pos);
   for (auto ix : tplan.node) A(C->tree.f() + ix);
