@@ -43,6 +43,24 @@ def test_proof_bytes_match_oracle(oracle, gpu_ctx, log_n, q, blowup, grind):
     assert rc == 0, err
 
 
+def test_grinding_windows_match_oracle(oracle, gpu_ctx):
+    """Grinding queues four ascending nonce windows per read-back (2^g, 2^g, 2^(g+1), 2^(g+2)
+    tries) and a window's kernel stops early only for a solution of an EARLIER window: over ten
+    seeds at grind 14 some nonces fall past the first window, and every proof (nonce, queries,
+    openings) must equal the oracle's sequential search (winterfell without `concurrent`)."""
+    import zkl_hip
+    oracle.set_threads(1)
+    n = 1 << 5
+    for k in range(10):
+        seed = 0x6B1D0000 + k
+        t, pi, w = zkl_hip.synth_vm_segment(seed, 5)
+        opts = zkl_hip.proof_options(w, n, queries=8, blowup=16, grind=14)
+        got = gpu_ctx.prove_segment(t, w, n, pi, opts)
+        ot, opi, _ = oracle.synth_segment(seed, 5)
+        want = oracle.prove(ot, w, n, opi, oracle.ProofOptions(*[getattr(opts, f) for f, _ in opts._fields_]))
+        assert got == want, f"seed {seed:#x}"
+
+
 @pytest.mark.parametrize("log_n,q,blowup,grind", [
     (5, 8, 16, 0), (6, 32, 8, 4), (8, 64, 16, 10), (10, 64, 16, 12), (7, 255, 8, 1),
 ])

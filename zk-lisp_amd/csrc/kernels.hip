@@ -585,6 +585,9 @@ __global__ PG_KERNEL void draw_kernel(fe seed, uint64_t base, size_t k, fe* out)
 
 __global__ PG_KERNEL void grind_kernel(fe seed, uint64_t base, uint32_t count, uint32_t bits,
                                                     unsigned long long* best) {
+  // an earlier window found one (every nonce of an earlier window is below base; a solution
+  // this window's other blocks have already found is not a reason to stop)
+  if (*(volatile unsigned long long*)best < base) return;
   PG_SETUP();
   const bool live = P.g < PG_PER_WAVE && item < count;
   const uint64_t nonce = base + item;
@@ -1406,6 +1409,9 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
   const size_t r0 = by_pos ? k : lde_pos(i * (N / ce), N, split);
   const size_t r1 = lde_pos((i * (N / ce) + c_ce.blowup) & (N - 1), N, split);
   auto cur = [&](int c) { return lde[(size_t)c * N + r0]; };
+  // next rows: position k + blowup for all but the rows whose L wraps; in the split layout
+  // they share the lines this wave's current rows just brought in (PMC: taking them from the
+  // neighbouring lane with ds_bpermute instead fetched the same bytes, round 3)
   auto nxt = [&](int c) { return lde[(size_t)c * N + r1]; };
   fe x = fe_mul(fe{3, 0}, roots[i << roots_shift]);
   const size_t per_period = ce / (c_ce.n / 32);

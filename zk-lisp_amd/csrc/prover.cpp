@@ -756,15 +756,24 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   if (o.grinding_factor == 0) {
     nonce = 1;
   } else {
-    // ascending windows of nonces, the minimum of the first window that holds a solution; the
-    // first window is 2^(g+1) tries (a solution with probability 1 - e^-2 = 0.86), so one
-    // launch and one read-back usually settle it
-    uint32_t batch = 1u << std::min<uint32_t>(std::max<uint32_t>(o.grinding_factor + 1, 14), 22);
-    for (uint64_t base = 1; nonce == 0; base += batch, batch = std::min<uint32_t>(batch * 2, 1u << 22)) {
+    // Ascending windows of nonces; the answer is the minimum of the first window that holds a
+    // solution.  Four windows (2^g, 2^g, 2^(g+1), 2^(g+2) tries) are queued per read-back, and
+    // a window's kernel returns at once when an earlier one has already found a solution
+    // (grind kernels check *best first), so the search costs the windows it needs plus a few
+    // empty launches, and one read-back settles it with probability 1 - e^-8.  A window of
+    // 2^16 tries is one permutation's latency on the chip (~0.45 ms); the expected cost is
+    // (1 + e^-1 + 2 e^-2 + 4 e^-4) windows = 1.7 instead of the 2.6 of one 2^(g+1) window first
+    // and doubling windows after it.
+    uint32_t batch = 1u << std::min<uint32_t>(std::max<uint32_t>(o.grinding_factor, 14), 22);
+    for (uint64_t base = 1; nonce == 0;) {
       unsigned long long init = ~0ull;
       HIPCHECK(hipMemcpyAsync(C->best.p, &init, 8, hipMemcpyHostToDevice, s));
       KScope k(C, KF_GRIND);
-      launch_grind(coin.seed, base, batch, o.grinding_factor, (unsigned long long*)C->best.p, s);
+      for (int w = 0; w < 4; w++) {
+        launch_grind(coin.seed, base, batch, o.grinding_factor, (unsigned long long*)C->best.p, s);
+        base += batch;
+        if (w >= 1) batch = std::min<uint32_t>(batch * 2, 1u << 22);
+      }
       check_launch("grinding");
       unsigned long long r = 0;
       d2h(C, &r, C->best.p, 8);
