@@ -806,3 +806,23 @@ def test_host_trace_chunked_upload_matches_device_entry(gpu_ctx, log_n, width_fl
         gpu_ctx.free(d)
     assert host == dev
     zkl_hip.verify_segment(host, pi, opts)
+
+
+@pytest.mark.parametrize("flags,blowup", [(0, 8), (0, 16), (0, 32), (0, 64), (1, 16), (2, 8)])
+def test_split_lde_layout_proofs_match_oracle(oracle, gpu_ctx, flags, blowup):
+    """2^8-row segments are the smallest whose trace LDE ends in an 8-stage register pass, so
+    the prover stores it in the split layout: blowup 8 puts every LDE row in the
+    CE domain (the evaluator reads all positions), 16 the even rows (first half only), 32 and 64
+    every 4th / 8th row (the evaluator walks CE points and looks rows up); sponge (flags 1) and
+    RAM/Merkle (flags 2) layouts add their AIR blocks.  Proof bytes equal the oracle's (natural
+    order throughout)."""
+    import zkl_hip
+    oracle.set_threads(1)
+    n = 1 << 8
+    seed = 0x5E1170 + 16 * flags + blowup
+    t, pi, w = zkl_hip.synth_vm_segment(seed, 8, flags)
+    opts = zkl_hip.proof_options(w, n, queries=32, blowup=blowup, grind=4)
+    got = gpu_ctx.prove_segment(t, w, n, pi, opts)
+    ot, opi, _ = oracle.synth_segment(seed, 8, flags)
+    want = oracle.prove(ot, w, n, opi, oracle.ProofOptions(*[getattr(opts, f) for f, _ in opts._fields_]))
+    assert got == want
