@@ -1388,13 +1388,24 @@ void launch_scale_bitrev(fe* d, size_t ncols, size_t n, const fe* scale, hipStre
 
 // POSE: the PoseidonAir block, RM: the RamAir / MerkleAir blocks; each is compiled into a
 // separate instance so that VM-only segments keep the smaller register footprint
+// CE_WAVES_CFG: occupancy target (waves per SIMD; 0 lets the compiler choose: 214 VGPRs, 2 waves
+// per SIMD for the VM-only instance).  The evaluator is latency-bound (dependent f128 products,
+// gathers of 2 x 204 columns): 3 waves per SIMD took it from 1.57 to 1.40 ms per proof and 4 to
+// 1.39 (round 3, profiles/r03/ab_ce); 3 keeps the larger Poseidon / RAM instances from spilling
+// much.
+#ifndef CE_WAVES_CFG
+#define CE_WAVES_CFG 3
+#endif
+#if CE_WAVES_CFG
+#define CE_OCC __attribute__((amdgpu_waves_per_eu(CE_WAVES_CFG, CE_WAVES_CFG)))
+#else
+#define CE_OCC
+#endif
 template <bool POSE, bool RM>
-__global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restrict__ lde, const fe* __restrict__ roots,
-                                                              int roots_shift, const fe* __restrict__ pertab,
-                                                              const fe* __restrict__ bm,
-                                                              const ProofConsts* __restrict__ K,
-                                                              const fe* __restrict__ xinv, fe* __restrict__ out,
-                                                              int split) {
+__device__ __forceinline__ void constraint_eval_body(const fe* __restrict__ lde, const fe* __restrict__ roots,
+                                                     int roots_shift, const fe* __restrict__ pertab,
+                                                     const fe* __restrict__ bm, const ProofConsts* __restrict__ K,
+                                                     const fe* __restrict__ xinv, fe* __restrict__ out, int split) {
   const AirDevice& c_air = K->air;
   const CeParams& c_ce = K->ce;
   const size_t ce = c_ce.ce, N = c_ce.N;
@@ -1430,6 +1441,27 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(const fe* __restri
   fe bsum2 = fe_sub_sel(reduce288(bacc), bm[(size_t)nb * ce + i]);
   fe v = fe_add_sel(fe_mul(tsum, x_gl), bsum2);
   out[i] = fe_mul(v, xn_inv);
+}
+
+// The VM-only and RAM / Merkle instances run at CE_WAVES_CFG waves per SIMD; the Poseidon
+// instances (90+ spilled VGPRs at 3 waves) keep the compiler's occupancy.
+template <bool RM>
+__global__ __launch_bounds__(256) CE_OCC void constraint_eval_kernel(const fe* __restrict__ lde, const fe* __restrict__ roots,
+                                                                    int roots_shift, const fe* __restrict__ pertab,
+                                                                    const fe* __restrict__ bm,
+                                                                    const ProofConsts* __restrict__ K,
+                                                                    const fe* __restrict__ xinv, fe* __restrict__ out,
+                                                                    int split) {
+  constraint_eval_body<false, RM>(lde, roots, roots_shift, pertab, bm, K, xinv, out, split);
+}
+template <bool RM>
+__global__ __launch_bounds__(256) void constraint_eval_pose_kernel(const fe* __restrict__ lde, const fe* __restrict__ roots,
+                                                                  int roots_shift, const fe* __restrict__ pertab,
+                                                                  const fe* __restrict__ bm,
+                                                                  const ProofConsts* __restrict__ K,
+                                                                  const fe* __restrict__ xinv, fe* __restrict__ out,
+                                                                  int split) {
+  constraint_eval_body<true, RM>(lde, roots, roots_shift, pertab, bm, K, xinv, out, split);
 }
 
 // out[i] = 1 / ((x_i - a1) (x_i - a2)^two) over the coset x_i = 3 w_M^i (w_M^i =
@@ -1472,13 +1504,13 @@ void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, con
   if (!xinv_ready) launch_coset_inv(d_roots, shift, p.ce, p.gl, fe_zero(), 0, d_xinv, s);
   const unsigned grid = (unsigned)((p.ce + 255) / 256);
   if (pose_block && ram_merkle)
-    constraint_eval_kernel<true, true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
+    constraint_eval_pose_kernel<true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
   else if (pose_block)
-    constraint_eval_kernel<true, false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
+    constraint_eval_pose_kernel<false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
   else if (ram_merkle)
-    constraint_eval_kernel<false, true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
+    constraint_eval_kernel<true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
   else
-    constraint_eval_kernel<false, false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
+    constraint_eval_kernel<false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
 }
 
 __global__ void boundary_scatter_kernel(const uint32_t* slot, const uint32_t* step, const fe* beta, size_t na, size_t n,
