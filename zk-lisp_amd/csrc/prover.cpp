@@ -310,6 +310,24 @@ void validate_request(uint32_t W, uint32_t n32, const zkl_air_public_inputs& pi,
 constexpr int UP_SLOTS = 4;
 constexpr size_t UP_SLOT_BYTES = (size_t)16 << 20;
 
+// host copy threads of the upload ring (ZKL_UP_THREADS, default 8) and ZKL_UP_MODE=direct (each
+// chunk straight from pageable memory; HIP stages it) for A/B on the GPU box
+static unsigned up_threads() {
+  static const unsigned t = [] {
+    const char* e = getenv("ZKL_UP_THREADS");
+    const unsigned d = std::max(1u, std::min(8u, std::thread::hardware_concurrency() / 2));
+    return e ? std::max(1, atoi(e)) : (int)d;
+  }();
+  return t;
+}
+static bool up_direct() {
+  static const bool d = [] {
+    const char* e = getenv("ZKL_UP_MODE");
+    return e && !strcmp(e, "direct");
+  }();
+  return d;
+}
+
 void parallel_copy(void* dst, const void* src, size_t bytes, unsigned nt) {
   if (nt <= 1 || bytes < ((size_t)1 << 20)) { memcpy(dst, src, bytes); return; }
   const size_t per = ((bytes + nt - 1) / nt + 63) & ~(size_t)63;
@@ -335,26 +353,42 @@ void upload_trace_chunked(zkl_ctx* C, const void* h_trace, uint32_t W, size_t n,
   const auto t0 = std::chrono::steady_clock::now();
   const size_t col_bytes = n * sizeof(fe);
   const uint32_t per = (uint32_t)std::max<size_t>(1, C->up_slot_bytes / col_bytes);
-  const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency() / 2));
+  const unsigned nt = up_threads();
+  const bool direct = up_direct();
   bool used[UP_SLOTS] = {false, false, false, false};
+  double copy_ms = 0, wait_ms = 0;
+  auto ms_since = [](std::chrono::steady_clock::time_point a) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+  };
   int k = 0;
   for (uint32_t c0 = 0; c0 < W; c0 += per, k = (k + 1) % UP_SLOTS) {
     const uint32_t nc = std::min(per, W - c0);
-    if (col_bytes * nc > C->up_slot_bytes) {  // one column larger than a slot: plain pageable copy
+    if (direct || col_bytes * nc > C->up_slot_bytes) {  // pageable copy (HIP stages it), or a column larger than a slot
       HIPCHECK(hipMemcpyAsync(C->coef.f() + (size_t)c0 * n, (const char*)h_trace + c0 * col_bytes, col_bytes * nc,
-                              hipMemcpyHostToDevice, s));
+                              hipMemcpyHostToDevice, direct ? C->up : s));
+      if (direct) {
+        HIPCHECK(hipEventRecord(C->up_ev[k], C->up));
+        HIPCHECK(hipStreamWaitEvent(s, C->up_ev[k], 0));
+      }
       on_chunk(c0, nc);
       continue;
     }
+    auto tw = std::chrono::steady_clock::now();
     if (used[k]) HIPCHECK(hipEventSynchronize(C->up_ev[k]));  // the slot's previous DMA has read it
+    wait_ms += ms_since(tw);
+    auto tc = std::chrono::steady_clock::now();
     parallel_copy(C->up_slot[k], (const char*)h_trace + c0 * col_bytes, col_bytes * nc, nt);
+    copy_ms += ms_since(tc);
     HIPCHECK(hipMemcpyAsync(C->coef.f() + (size_t)c0 * n, C->up_slot[k], col_bytes * nc, hipMemcpyHostToDevice, C->up));
     HIPCHECK(hipEventRecord(C->up_ev[k], C->up));
     used[k] = true;
     HIPCHECK(hipStreamWaitEvent(s, C->up_ev[k], 0));
     on_chunk(c0, nc);
   }
-  C->up_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  C->up_ms = ms_since(t0);
+  if (getenv("ZKL_UP_DEBUG"))
+    fprintf(stderr, "[zkl upload] %u cols x %zu rows: loop %.2f ms (host copy %.2f ms on %u threads, slot waits %.2f ms)%s\n",
+            W, n, C->up_ms, copy_ms, nt, wait_ms, direct ? " direct" : "");
 }
 
 // proofs running in any context: the row-digest rule (a process-wide test switch, DESIGN.md
