@@ -15,7 +15,8 @@
 //                                Proof::to_bytes out (the call at prove.rs:1142)
 //   zkl::verify_proof            verify_proof (prove.rs:802-941), one segment
 //   zkl::StepProof               proof::step::StepProof::to_bytes / digest (step.rs:79-151,
-//                                digest.rs:16-68), children_root (agg/child.rs:853-895)
+//                                digest.rs:16-68), step_meta_for (prove.rs:1103-1174),
+//                                children_root (agg/child.rs:853-895)
 //   zkl::WinterfellBackend       RecursionBackend::prove / verify (lib.rs:295-372): the
 //                                aggregation proof and its ZKLRC1 artifact
 //   zkl::Error                   prove::Error (prove.rs:51-60): Backend(String) for prover and
@@ -208,6 +209,36 @@ class ZkProver {
 // failing check
 inline void verify_proof(const Proof& proof, const AirPublicInputs& pi, const ProofOptions& opts) {
   detail::check(zkl_verify_segment(proof.bytes.data(), proof.bytes.size(), &pi, &opts.raw()));
+}
+
+// zl1 step metadata as prove_segment fills it (prove.rs:1103-1174): suite = program_id
+// (prove.rs:985), the boundary bytes fe_to_bytes_fold of the AIR public inputs' pc_init, RAM
+// grand products and ROM lanes (SegmentBoundaryBytes, prove.rs:1112), the segment position and
+// the VM state hashes of the trace builder.  Typed main args (pi.rs VmArg) go in meta.main_args.
+inline zkl_step_info step_meta_for(const AirPublicInputs& pi, uint32_t index, uint32_t total, const Digest& state_in,
+                                   const Digest& state_out, uint32_t lambda_bits = 128) {
+  zkl_step_info m;
+  std::memset(&m, 0, sizeof m);
+  std::memcpy(m.suite_id, pi.program_id, 32);
+  m.lambda_bits = lambda_bits;
+  m.segment_index = index;
+  m.segments_total = total;
+  auto fold = [](const BaseElement& v, uint8_t out[32]) {  // 16 LE bytes of the value, 16 zero
+    for (int i = 0; i < 8; i++) out[i] = (uint8_t)(v.lo >> (8 * i));
+    for (int i = 0; i < 8; i++) out[8 + i] = (uint8_t)(v.hi >> (8 * i));
+  };
+  fold(pi.pc_init, m.pc_init);
+  std::memcpy(m.state_in_hash, state_in.data(), 32);
+  std::memcpy(m.state_out_hash, state_out.data(), 32);
+  fold(pi.ram_gp_unsorted_in, m.ram_gp_unsorted_in);
+  fold(pi.ram_gp_unsorted_out, m.ram_gp_unsorted_out);
+  fold(pi.ram_gp_sorted_in, m.ram_gp_sorted_in);
+  fold(pi.ram_gp_sorted_out, m.ram_gp_sorted_out);
+  for (int i = 0; i < 3; i++) {
+    fold(pi.rom_s_in[i], m.rom_s_in[i]);
+    fold(pi.rom_s_out[i], m.rom_s_out[i]);
+  }
+  return m;
 }
 
 // zl1 step proof (proof/step.rs, proof/format.rs, proof/digest.rs)

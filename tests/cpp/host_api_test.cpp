@@ -101,12 +101,9 @@ int run_gpu(const char* out_path) {
   bad.bytes[bad.bytes.size() / 2] ^= 1;
   EXPECT(throws_backend([&] { zkl::verify_proof(bad, s.pi, opts); }, nullptr));
   // zl1 step + aggregation of the one-segment program (RecursionBackend::prove / verify)
-  zkl_step_info meta{};
-  std::memcpy(meta.suite_id, s.pi.program_id, 32);
-  meta.lambda_bits = 128;
-  meta.segment_index = 0;
-  meta.segments_total = 1;
-  meta.state_out_hash[0] = 1;
+  zkl::Digest s_in{}, s_out{};
+  s_out[0] = 1;
+  const zkl_step_info meta = zkl::step_meta_for(s.pi, 0, 1, s_in, s_out);
   const zkl::StepProof step = zkl::StepProof::from_inner(s.pi, meta, proof);
   const auto dr = step.digest();
   zkl::Digest suite{};
