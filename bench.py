@@ -15,8 +15,11 @@ processes of itself with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 
 set, relays rank 0's JSON line and exits non-zero if any rank fails.  Rank r proves segment
 seed 0x5EED0001 + r on device LOCAL_RANK (ZKL_BENCH_DEVICE pins every rank to one device to
 rehearse N ranks on fewer GPUs; the JSON line then says so).  Weak scaling, no data-path
-collective; the barrier, max-over-ranks timing and the step-proof hand-off
-use torch.distributed's gloo backend on host memory (zkl_hip/dist.py).
+collective.  The step-proof hand-off to rank 0 runs over RCCL (zkl_comm_*,
+ncclSend/ncclRecv over xGMI); with one GPU per rank RCCL is required, and a failure to start it
+or to gather ends the run non-zero.  gloo carries the barrier, the max-over-ranks timing and the
+RCCL unique id, and carries the step bytes only in a same-device rehearsal (ZKL_BENCH_DEVICE) or
+with ZKL_COMM=gloo, which the line's handoff.transport states (zkl_hip/dist.py).
 
 Parity.  Every rank hashes its last proof and compares it with the committed CPU-oracle
 golden of its segment (tests/golden/proof_2p16.json, make_proof_goldens.py); at N = 1 the
@@ -24,8 +27,10 @@ cpu_baseline leg also proves the same segment on the oracle and compares the byt
 
 Other lines: configs[2] (8 distinct segments on one GPU, 1/2/4 contexts in flight), configs[3]
 shape (--segments S distinct segments sharded over the ranks, each rank pipelining its share,
-then the step-proof gather and children root on rank 0; default S = 8 x N when N > 1) and
-configs[4] (one 2^20-row segment).  Device synchronisation is zkl_hip_synchronize
+then the step-proof gather and children root on rank 0; default S = 8 x N when N > 1),
+configs[4] (one 2^20-row segment per rank: replicas, max-over-ranks time) and the real program
+examples/rollup-bench.zlisp at --max-segment-rows 65536 (one 65,536-row x 212-column segment
+built from the compiler's op list, tests/golden/programs.json; N = 1).  Device synchronisation is zkl_hip_synchronize
 (hipDeviceSynchronize) on both sides of every timed region.
 """
 import argparse
@@ -45,6 +50,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SEED0 = 0x5EED0001             # segment seed of rank / segment 0
 GOLDEN = os.path.join(ROOT, "tests", "golden", "proof_2p16.json")
 CHAIN = os.path.join(ROOT, "tests", "golden", "chain_2p16.json")  # the multi-segment program (make_chain_goldens.py)
+PROGRAMS = os.path.join(ROOT, "tests", "golden", "programs.json")  # real .zlisp programs (make_programs.py)
 VALU_MIX = os.path.join(ROOT, "profiles", "r02", "valu_mix.json")
 VALU_FLOOR = os.path.join(ROOT, "profiles", "r03", "valu_floor.json")
 ROW_KERNEL = {"mfma": "hash_rows_pm_kernel<0>", "lane": "hash_rows_kernel<0>"}
@@ -293,27 +299,107 @@ def spawn_ranks(n):
     return 0
 
 
+def lines_for_rank(args, world):
+    """The bench lines every rank takes part in (the --dry-run report; main() runs the same)."""
+    lines = ["headline", "step_handoff"]
+    n_seg = args.segments if args.segments >= 0 else (8 * world if world > 1 else 0)
+    if n_seg > 0:
+        lines.append("c4_sharded")
+    if args.c5_log_n > 0:
+        lines.append("c5_single_segment")
+    if world == 1:
+        lines += [x for x, on in (("host_trace", args.host_steps > 0), ("c3_in_gpu_pipeline", args.c3_segments > 0),
+                                  ("real_program", args.program_steps > 0),
+                                  ("cpu_baseline", not args.no_cpu_baseline)) if on]
+    return lines
+
+
 # ------------------------------------------------------------------------ workloads
-def c5_single(zkl_hip, device, log_n):
+def c5_single(zkl_hip, device, log_n, barrier=lambda: None, seed=0x5EED0C05):
     """BASELINE configs[4] shape on one GPU: one synthetic 2^log_n-row segment (blowup 16,
-    q 64, grind 16, partitions (16,16) at 2^20 rows), trace resident in HBM; on 8 GPUs each
-    rank proves its own segment (replicas).  One warm-up proof, one timed.
-    Returns (ms per proof, proof bytes)."""
+    q 64, grind 16, partitions (16,16) at 2^20 rows), trace resident in HBM; on N GPUs every
+    rank proves its own segment (replicas) between barriers.  One warm-up proof,
+    one timed.  Every rank passes both barriers even if its own setup or proof fails, so a
+    failing rank cannot leave the others waiting.  Returns (ms per proof, proof bytes, error)."""
     n = 1 << log_n
-    ctx = zkl_hip.Context(device)
-    t, pi, w = zkl_hip.synth_vm_segment(0x5EED0C05, log_n)
-    d = ctx.alloc(w * n * 16)
-    ctx.upload(d, t, w * n * 16)
+    ctx = d = None
+    err = ms = nbytes = None
+    try:
+        ctx = zkl_hip.Context(device)
+        t, pi, w = zkl_hip.synth_vm_segment(seed, log_n)
+        d = ctx.alloc(w * n * 16)
+        ctx.upload(d, t, w * n * 16)
+        del t
+        o = zkl_hip.proof_options(w, n)
+        ctx.prove_segment_device(d, w, n, pi, o)
+        ctx.synchronize()
+    except Exception as e:  # noqa: BLE001  (reported in the line)
+        err = str(e)
+    barrier()
+    if err is None:
+        try:
+            t0 = time.perf_counter()
+            proof = ctx.prove_segment_device(d, w, n, pi, o)
+            ctx.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3
+            nbytes = len(proof)
+        except Exception as e:  # noqa: BLE001
+            err = str(e)
+    barrier()
+    if ctx is not None:
+        if d is not None:
+            ctx.free(d)
+        ctx.close()
+    return ms, nbytes, err
+
+
+def real_program(zkl_hip, device, steps, name="rollup-bench", max_rows=1 << 16):
+    """The reference's own example program at the metric's shape: `zk-lisp prove
+    examples/<name>.zlisp --max-segment-rows 65536` with the CLI's arguments.  The op list is
+    the compiler's (tests/golden/programs.json, lowered by oracle/lower_ref.py from the source
+    and committed as data); the product builds the trace (zkl_build_trace), plans and slices the
+    segment (zkl_plan_segments / zkl_slice_segment: one 65,536-row segment, {vm, ram, sponge,
+    rom} layout, 212 columns), uploads it and proves it `steps` times resident in HBM.  The
+    proof bytes are compared with the oracle's golden."""
+    tab = json.load(open(PROGRAMS))[name]
+    plan_g = tab["plans"][str(max_rows)]
+    ops = [zkl_hip.op(k, **f) for k, f in tab["ops"]]
+    main_args = [(tg, bytes.fromhex(b)) for tg, b in tab["cli"]["main_args"]]
+    t, pi, w, n = zkl_hip.build_trace(ops, bytes.fromhex(tab["program_id"]), secret_args=tab["cli"]["secret_u64"],
+                                      main_args=main_args)
+    plan = zkl_hip.plan_segments(len(ops), max_rows)
+    if [list(p) for p in plan] != [s["rows"] for s in plan_g["segments"]] or len(plan) != 1:
+        raise RuntimeError(f"{name}: plan {plan} differs from the golden plan")
+    a, b = plan[0]
+    st, spi, sw, _, _ = zkl_hip.slice_segment(t, w, n, ops, pi, a, b)
     del t
-    o = zkl_hip.proof_options(w, n)
-    ctx.prove_segment_device(d, w, n, pi, o)
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    proof = ctx.prove_segment_device(d, w, n, pi, o)
-    ms = (time.perf_counter() - t0) * 1e3
-    ctx.free(d)
-    ctx.close()
-    return ms, len(proof)
+    m = b - a
+    cli = tab["cli"]
+    o = zkl_hip.proof_options(sw, m, queries=cli["queries"], blowup=cli["blowup"], grind=cli["grind"])
+    ctx = zkl_hip.Context(device)
+    d = ctx.alloc(sw * m * 16)
+    ctx.upload(d, st, sw * m * 16)
+    del st
+    try:
+        ctx.prove_segment_device(d, sw, m, spi, o)
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            proof = ctx.prove_segment_device(d, sw, m, spi, o)
+        ctx.synchronize()
+        dt = time.perf_counter() - t0
+    finally:
+        ctx.free(d)
+        ctx.close()
+    want = plan_g["segments"][0]["proof_sha256"]
+    got = hashlib.sha256(proof).hexdigest()
+    return {"config": f"examples/{name}.zlisp (--arg u64:10 --arg bytes32:0x01), --max-segment-rows {max_rows}: "
+                      f"one {m}-row x {sw}-column segment (feature mask {spi.segment_feature_mask:#x}: vm, ram, "
+                      f"sponge, rom), blowup {cli['blowup']}, q {cli['queries']}, grind {cli['grind']}, "
+                      f"partitions ({o.num_partitions},{o.hash_rate}); op list from the compiler restatement",
+            "value": round(steps / dt, 4), "unit": "segment-proofs/s", "ms_per_proof": round(dt / steps * 1e3, 3),
+            "steps": steps, "rows": m, "width": sw, "proof_bytes": len(proof),
+            "parity": "match" if got == want else "MISMATCH", "golden": "tests/golden/programs.json (CPU oracle)"}
 
 
 class Pipeline:
@@ -438,7 +524,7 @@ def handoff(zkl_hip, dist, items, total, chained=False, device=0):
         out["transport"] = "rccl (ncclAllGather of lengths + ncclSend/ncclRecv to rank 0)"
         out["rccl_device_ms"] = round(comm.last_ms(), 3)
     else:
-        out["transport"] = f"gloo (RCCL unavailable: {cerr})"
+        out["transport"] = f"gloo ({cerr})"
     return out, [d["raw"] for d in steps]
 
 
@@ -458,6 +544,8 @@ def main():
                     help="configs[3] shape: distinct segments sharded over the ranks (-1: 8 x N when N > 1, else 0)")
     ap.add_argument("--inflight", type=int, default=4, help="contexts in flight per rank for --segments")
     ap.add_argument("--c5-log-n", type=int, default=20, help="rows (log2) of the configs[4] single-segment line (0: skip)")
+    ap.add_argument("--program-steps", type=int, default=5,
+                    help="proofs of the real rollup-bench.zlisp 65,536-row segment (N = 1; 0: skip)")
     ap.add_argument("--host-steps", type=int, default=5,
                     help="proofs timed through zkl_hip_prove_segment with a host-resident trace (N = 1; 0: skip)")
     ap.add_argument("--dry-run", action="store_true", help="launcher / rank plumbing only, no device work (CPU tests)")
@@ -490,10 +578,12 @@ def main():
         dist.barrier()
         elapsed = dist.max_over_ranks(time.perf_counter() - t0)
         mine = dist.segments_for_rank(n_seg, rank, world)
-        got = dist.gather_to_root({"rank": rank, "segments": mine})
+        got = dist.gather_to_root({"rank": rank, "segments": mine, "lines": lines_for_rank(args, world)})
         if rank == 0:
             print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "dry_run": True,
-                              "elapsed_s": elapsed, "segments_by_rank": {g["rank"]: g["segments"] for g in got}}),
+                              "elapsed_s": elapsed, "segments_by_rank": {g["rank"]: g["segments"] for g in got},
+                              "lines_by_rank": {g["rank"]: g["lines"] for g in got},
+                              "rccl_required": dist.rccl_required()}),
                   file=result_out, flush=True)
         dist.shutdown()
         return 0
@@ -600,6 +690,27 @@ def main():
             if c4["golden_mismatches"] or "error" in c4["aggregation"] or c4["aggregation"].get("golden") == "MISMATCH":
                 failures.append("c4_sharded")
 
+    # configs[4]: one 2^20-row segment per rank (replicas), timed between barriers
+    c5 = None
+    if args.c5_log_n > 0:
+        dist.barrier()
+        ms5, pb5, err5 = c5_single(zkl_hip, device, args.c5_log_n, barrier=dist.barrier, seed=0x5EED0C05 + rank)
+        if err5 is not None:
+            err5 = f"rank {rank}: {err5}"
+            log(err5)
+        errs5 = [e for e in (dist.gather_to_root(err5) or []) if e]
+        ms5 = dist.max_over_ranks(ms5 if ms5 is not None else float("inf"))
+        if rank == 0:
+            if errs5:
+                c5 = {"error": "; ".join(errs5)}
+            else:
+                c5 = {"config": f"BASELINE configs[4] shape: one synthetic 2^{args.c5_log_n}-row segment per rank "
+                                f"(blowup 16, q 64, grind 16, partitions (16,16)) on {world} GPU(s): replicas, "
+                                "each rank its own segment, max-over-ranks time",
+                      "value": round(world / (ms5 * 1e-3), 4), "unit": "segment-proofs/s",
+                      "ms_per_proof": round(ms5, 1), "proof_bytes": pb5,
+                      "rows_per_s": round(world * (1 << args.c5_log_n) / ms5 * 1e3)}
+
     if rank == 0:
         value = world * args.steps / elapsed
         dom = max(fam.items(), key=lambda kv: kv[1][0])[0] if fam else "trace_hash_rows"
@@ -697,17 +808,18 @@ def main():
             a3 = out["c3_in_gpu_pipeline"]["aggregation"]
             if c3_par["golden_mismatches"] or "error" in a3 or a3.get("golden") == "MISMATCH":
                 failures.append("c3_in_gpu_pipeline")
-        if world == 1 and args.c5_log_n > 0:
-            try:
-                ms5, pb5 = c5_single(zkl_hip, device, args.c5_log_n)
-                out["c5_single_segment"] = {
-                    "config": f"BASELINE configs[4] shape on one GPU: one synthetic 2^{args.c5_log_n}-row segment, "
-                              "blowup 16, q 64, grind 16 (each of the 8 GPUs proves its own)",
-                    "ms_per_proof": round(ms5, 1), "proof_bytes": pb5,
-                    "rows_per_s": round((1 << args.c5_log_n) / ms5 * 1e3)}
-            except Exception as e:  # reported in the line, and the run exits non-zero
-                out["c5_single_segment"] = {"error": str(e)}
+        if c5 is not None:
+            out["c5_single_segment"] = c5
+            if "error" in c5:
                 failures.append("c5_single_segment")
+        if world == 1 and args.program_steps > 0:
+            try:
+                out["real_program"] = real_program(zkl_hip, device, args.program_steps)
+                if out["real_program"]["parity"] != "match":
+                    failures.append("real_program")
+            except Exception as e:  # reported in the line, and the run exits non-zero
+                out["real_program"] = {"error": str(e)}
+                failures.append("real_program")
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(args.cpu_sample_log_n or log_n, cpu_threads(args.cpu_threads),

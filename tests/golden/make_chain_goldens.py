@@ -20,11 +20,18 @@ VM state hashes are state_in(i) = i, state_out(i) = i + 1 (32-byte LE).  The fil
     count, hash_row_poseidon root errors) over the 16 first segments, whose
     trace has 16 rows like the published run's (its agg proof was 52,558 B).
 
+  * "aggregation_64_ref_trace": the reference-trace mode over all 64 segments (64-row trace).
+
 Proof bytes are cached per segment under .chain_cache/ (git- and gpurun-ignored) so the run can
 be resumed; each proof is checked by the oracle verifier before it is used.
 
 Run (build container, ~2-3 min per proof on 8 threads; ~2.5 h for all 64):
     python tests/golden/make_chain_goldens.py [--threads 8] [--segments 64]
+
+Add only the aggregation entries, from proof bytes already at hand -- e.g. the GPU test's dump
+(ZKL_DUMP_CHAIN=<dir> test_chain_64_segments_and_aggregation_match_goldens): every file must
+hash to the committed oracle sha256 of its segment, so the inputs are the oracle's proofs:
+    python tests/golden/make_chain_goldens.py --from-dir <dir>
 """
 import argparse
 import ctypes as C
@@ -71,6 +78,26 @@ def agg_entry(steps, mode=0):
             "len": len(art), "sha256": hashlib.sha256(art).hexdigest(), "recursion_digest": dg.hex()}
 
 
+def from_dir(d):
+    """Aggregation entries from 64 proof files that hash to the committed segment goldens."""
+    out = json.load(open(OUT))
+    pis, proofs = [], []
+    for i in range(SEGMENTS):
+        g = out["segments"][i]
+        proof = open(os.path.join(d, f"seg{i:02d}.bin"), "rb").read()
+        assert g["index"] == i and hashlib.sha256(proof).hexdigest() == g["sha256"], f"segment {i} differs from its golden"
+        _, pi, _ = oracle_lib.synth_segment_chain(PROGRAM, PROGRAM + i, LOG_N, int(out["rom0_in"][i], 16))
+        pis.append(pi)
+        proofs.append(proof)
+    for key, k, mode in (("aggregation", PINNED8, 0), ("aggregation_ref_trace", REF_TRACE_CHILDREN, 1),
+                         ("aggregation_64", SEGMENTS, 0), ("aggregation_64_ref_trace", SEGMENTS, 1)):
+        e = agg_entry(steps_for(pis, proofs, k), mode=mode)
+        if key in out:
+            assert out[key] == e, f"{key}: recomputed entry differs from the committed one"
+        out[key] = e
+    json.dump(out, open(OUT, "w"), indent=1, sort_keys=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=min(8, os.cpu_count() or 1))
@@ -78,7 +105,10 @@ def main():
     ap.add_argument("--skip-agg", action="store_true")
     ap.add_argument("--start", type=int, default=0, help="with --skip-agg: first segment to prove")
     ap.add_argument("--stop", type=int, default=SEGMENTS, help="with --skip-agg: one past the last segment")
+    ap.add_argument("--from-dir", default=None, help="seg{i:02d}.bin proofs matching the committed hashes")
     args = ap.parse_args()
+    if args.from_dir:
+        return from_dir(args.from_dir)
     oracle_lib.set_threads(args.threads)
     os.makedirs(CACHE, exist_ok=True)
     n = 1 << LOG_N

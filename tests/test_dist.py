@@ -50,7 +50,8 @@ def _step_worker(rank, world, port, q):
     import zkl_hip
     from zkl_hip import dist
     dist.init()
-    comm, cerr = dist.init_rccl(0)  # no GPU here: every rank gets the same error, gloo carries the bytes
+    # no GPU here: every rank gets the same error, and with required=False gloo carries the bytes
+    comm, cerr = dist.init_rccl(0, required=False)
     t, opi, w = oracle_lib.synth_segment(0x5EED7000 + rank, 5)
     inner = oracle_lib.prove(t, w, 32, opi, oracle_lib.default_options(w, 32, queries=4, grind=0))
     pi = zkl_hip.AirPublicInputs()
@@ -101,6 +102,73 @@ def test_gloo_step_handoff_world_size_2():
     assert (steps[0][1], steps[0][2]) == res[0][1] and (steps[1][1], steps[1][2]) == res[1][1]
     assert root == zkl_hip.children_root(suite, [s[1] for s in steps], [s[2] for s in steps])
     assert root != bytes(32)
+
+
+def _required_worker(rank, world, port, q, pinned):
+    """init_rccl with the default policy: one GPU per rank (no ZKL_BENCH_DEVICE) requires RCCL,
+    so with no GPU every rank raises; a same-device rehearsal falls back to gloo, labelled."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    os.environ.pop("ZKL_COMM", None)
+    if pinned:
+        os.environ["ZKL_BENCH_DEVICE"] = "0"
+    else:
+        os.environ.pop("ZKL_BENCH_DEVICE", None)
+    sys.path.insert(0, os.path.join(ROOT, "zk-lisp_amd"))
+    from zkl_hip import dist
+    dist.init()
+    try:
+        comm, err = dist.init_rccl(0)
+        res = ("fallback", comm is None, err)
+    except RuntimeError as e:
+        res = ("raised", None, str(e))
+    q.put((rank, dist.rccl_required(), res))
+    dist.shutdown()
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_rccl_required_with_one_gpu_per_rank(pinned):
+    """with one GPU per rank a failed RCCL start raises on every rank (the
+    bench then exits non-zero) instead of silently degrading to gloo; a same-device rehearsal
+    (ZKL_BENCH_DEVICE) keeps gloo and says so."""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_required_worker, args=(r, 2, port, q, pinned)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (req, x)) for r, req, x in (q.get(timeout=180) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        req, (kind, none, msg) = res[r]
+        assert req is (not pinned)
+        if pinned:
+            assert kind == "fallback" and none and "same-device rehearsal" in msg
+        else:
+            assert kind == "raised" and "RCCL hand-off required" in msg
+
+
+def test_bench_dry_run_reports_lines_and_transport_policy():
+    """--dry-run at N = 2: every rank runs the configs[4] replica line (c5_single_segment) and
+    the sharded configs[3] line; the RCCL hand-off is required with one GPU per rank and not in
+    a same-device rehearsal."""
+    import json
+    for env, req in (({}, True), ({"ZKL_BENCH_DEVICE": "0"}, False), ({"ZKL_COMM": "gloo"}, False)):
+        r = _bench(["--gpus", "2", "--dry-run"], env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+        assert out["rccl_required"] is req
+        for rank in ("0", "1"):
+            lines = out["lines_by_rank"][rank]
+            assert "c5_single_segment" in lines and "c4_sharded" in lines and "real_program" not in lines
+    r = _bench(["--gpus", "1", "--dry-run"])
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["rccl_required"] is False and "real_program" in out["lines_by_rank"]["0"]
 
 
 def test_step_chain_check_rejects_broken_chain():

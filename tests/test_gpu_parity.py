@@ -694,7 +694,7 @@ def _chain():
 def _prove_chain(K, inflight=4):
     """The first K segments of the synthetic chained program, proved on the GPU by `inflight`
     contexts (one host thread each, the reference's bounded segment pool prove.rs:1018-1050),
-    wrapped as zl1 steps of a K-segment program.  Returns (proofs, steps)."""
+    wrapped as zl1 steps of a K-segment program.  Returns (proofs, steps, public inputs)."""
     import threading
     import zkl_hip
     ch = _chain()
@@ -730,7 +730,7 @@ def _prove_chain(K, inflight=4):
     for i, (pi, p) in enumerate(zip(pis, got)):
         info = zkl_hip.step_info_for(pi, i, K, i.to_bytes(32, "little"), (i + 1).to_bytes(32, "little"))
         steps.append(zkl_hip.step_proof_encode(pi, info, p))
-    return got, steps
+    return got, steps, pis
 
 
 def _check_segments(got):
@@ -752,7 +752,7 @@ def test_chain_program_and_aggregation_match_goldens(oracle, gpu_ctx):
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
     import agg_ref
     ch = _chain()
-    got, steps = _prove_chain(8)
+    got, steps, _ = _prove_chain(8)
     _check_segments(got)
     art, dg = zkl_hip.agg_prove(steps)
     ga = ch["aggregation"]
@@ -771,11 +771,22 @@ def test_chain_64_segments_and_aggregation_match_goldens(gpu_ctx):
     1050), 4 contexts in flight, equal the 64 oracle goldens; the 64 zl1 steps aggregate
     (lib.rs:295-551) into the golden 64-child ZKLRC1 artifact (oracle/agg_ref.py over the
     oracle's step proofs) and recursion digest, and the product verifier accepts it.  The
-    8-GPU run shards exactly these segments (bench.py --gpus 8, zkl_hip/dist.py)."""
+    8-GPU run shards exactly these segments (bench.py --gpus 8, zkl_hip/dist.py).
+
+    The reference-trace aggregation mode (agg/trace.rs:397-398 row count, hash_row_poseidon
+    root errors 553-600) at real size: the first 16 segments as a 16-step program give the
+    golden `aggregation_ref_trace` artifact (16-row trace, like the published run's), and all 64
+    give `aggregation_64_ref_trace` (64 rows: no padding row).  With ZKL_DUMP_CHAIN=<dir> the
+    proof bytes are written there (make_chain_goldens.py --from-dir uses them)."""
     import zkl_hip
     ch = _chain()
-    got, steps = _prove_chain(64)
+    got, steps, pis = _prove_chain(64)
     _check_segments(got)
+    dump = os.environ.get("ZKL_DUMP_CHAIN")
+    if dump:
+        os.makedirs(dump, exist_ok=True)
+        for i, p in enumerate(got):
+            open(os.path.join(dump, f"seg{i:02d}.bin"), "wb").write(p)
     art, dg = zkl_hip.agg_prove(steps)
     ga = ch["aggregation_64"]
     assert ga["children"] == 64
@@ -784,6 +795,19 @@ def test_chain_64_segments_and_aggregation_match_goldens(gpu_ctx):
     zkl_hip.agg_verify(art)
     T = zkl_hip.agg_trace(steps)
     assert len(T[0]) == 128  # next_pow2(max(64 + 1, 8)): the padding row
+    ref16 = []
+    for i in range(16):  # the first 16 proofs as steps of a 16-segment program
+        pi = pis[i]
+        info = zkl_hip.step_info_for(pi, i, 16, i.to_bytes(32, "little"), (i + 1).to_bytes(32, "little"))
+        ref16.append(zkl_hip.step_proof_encode(pi, info, got[i]))
+    for key, st, rows in (("aggregation_ref_trace", ref16, 16), ("aggregation_64_ref_trace", steps, 64)):
+        g = ch.get(key)
+        if g is None:
+            continue
+        art, dg = zkl_hip.agg_prove(st, trace_mode=zkl_hip.AGG_TRACE_REFERENCE)
+        assert g["children"] == len(st)
+        assert (len(art), hashlib.sha256(art).hexdigest(), dg.hex()) == (g["len"], g["sha256"], g["recursion_digest"]), key
+        assert len(zkl_hip.agg_trace(st, trace_mode=zkl_hip.AGG_TRACE_REFERENCE)[0]) == rows
 
 
 @pytest.mark.parametrize("log_n,width_flags", [(16, 0), (18, 0), (12, 2)])

@@ -86,7 +86,7 @@ def test_lowering_restatement_cases():
     assert ops == [("Mov", {"dst": 7, "src": 1}), ("Const", {"dst": 6, "imm": 1}), ("Sub", {"dst": 7, "a": 7, "b": 6}),
                    ("Mov", {"dst": 0, "src": 7}), ("End", {})]
     with pytest.raises(NotImplementedError):
-        lower_ref.compile_entry("(def (main) (hash2 1 2))", [])
+        lower_ref.compile_entry("(def (main) (merkle-verify 1 2))", [])
     with pytest.raises(ValueError):
         lower_ref.compile_entry("(def (main x) x)", [])
 

@@ -91,9 +91,38 @@ struct zkl_comm {
   void* d_buf = nullptr;   // world x cap bytes (this rank's blob in slot `rank`)
   size_t cap = 0;
   double last_ms = 0;      // device time of the last gather (HIP events on the comm stream)
+  bool broken = false;     // a failed collective leaves peers mid-call: the comm is not reused
 };
 
 namespace {
+// RAII for the two timing events and the RCCL group of one gather: an exception between
+// ncclGroupStart and ncclGroupEnd still closes the group, and the events never leak.
+struct Events {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  Events() {
+    ZKL_HIPCHECK(hipEventCreate(&e0));
+    ZKL_HIPCHECK(hipEventCreate(&e1));
+  }
+  ~Events() {
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+  }
+};
+struct Group {
+  bool open = false;
+  void start() {
+    nccl_check(rccl().GroupStart(), "ncclGroupStart");
+    open = true;
+  }
+  void end() {
+    open = false;
+    nccl_check(rccl().GroupEnd(), "ncclGroupEnd");
+  }
+  ~Group() {
+    if (open) (void)rccl().GroupEnd();
+  }
+};
+
 void ensure_cap(zkl_comm* c, size_t need) {
   if (need <= c->cap) return;
   if (c->d_buf) (void)hipFree(c->d_buf);
@@ -146,15 +175,17 @@ int zkl_comm_init(int device, int world, int rank, const uint8_t id[128], zkl_co
 int zkl_comm_gather_bytes(zkl_comm* c, const uint8_t* data, size_t len, int root, uint8_t** out, size_t* lens_out) {
   if (!c || (!data && len) || root < 0 || root >= c->world) return ZKL_E_INVALID;
   if (c->rank == root && (!out || !lens_out)) return ZKL_E_INVALID;
+  if (c->broken)
+    return zkl::guarded_call([] {
+      throw std::runtime_error("zkl_comm_gather_bytes: the communicator failed in an earlier collective; destroy it");
+    });
   std::vector<uint8_t> host;
   std::vector<uint64_t> lens(c->world, 0);
   const int rc = zkl::guarded_call([&] {
     const Rccl& R = rccl();
     ZKL_HIPCHECK(hipSetDevice(c->device));
-    hipEvent_t e0, e1;
-    ZKL_HIPCHECK(hipEventCreate(&e0));
-    ZKL_HIPCHECK(hipEventCreate(&e1));
-    ZKL_HIPCHECK(hipEventRecord(e0, c->stream));
+    Events ev;
+    ZKL_HIPCHECK(hipEventRecord(ev.e0, c->stream));
     // 1. every rank learns every blob length (one u64 per rank)
     const uint64_t mine = len;
     uint8_t* d_lens = (uint8_t*)c->d_lens;
@@ -171,7 +202,8 @@ int zkl_comm_gather_bytes(zkl_comm* c, const uint8_t* data, size_t len, int root
     uint8_t* slot = (uint8_t*)c->d_buf + c->cap * (size_t)c->rank;
     if (len) ZKL_HIPCHECK(hipMemcpyAsync(slot, data, len, hipMemcpyHostToDevice, c->stream));
     // 2. point-to-point to the root, one transfer per rank, grouped so they progress together
-    nccl_check(R.GroupStart(), "ncclGroupStart");
+    Group group;
+    group.start();
     if (c->rank == root) {
       for (int r = 0; r < c->world; r++)
         if (r != root && lens[r])
@@ -180,8 +212,8 @@ int zkl_comm_gather_bytes(zkl_comm* c, const uint8_t* data, size_t len, int root
     } else if (len) {
       nccl_check(R.Send(slot, len, ncclUint8, root, c->comm, c->stream), "ncclSend");
     }
-    nccl_check(R.GroupEnd(), "ncclGroupEnd");
-    ZKL_HIPCHECK(hipEventRecord(e1, c->stream));
+    group.end();
+    ZKL_HIPCHECK(hipEventRecord(ev.e1, c->stream));
     if (c->rank == root) {
       size_t tot = 0;
       for (uint64_t l : lens) tot += (size_t)l;
@@ -196,12 +228,13 @@ int zkl_comm_gather_bytes(zkl_comm* c, const uint8_t* data, size_t len, int root
     }
     ZKL_HIPCHECK(hipStreamSynchronize(c->stream));
     float ms = 0;
-    ZKL_HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+    ZKL_HIPCHECK(hipEventElapsedTime(&ms, ev.e0, ev.e1));
     c->last_ms = ms;
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
   });
-  if (rc) return rc;
+  if (rc) {
+    c->broken = true;
+    return rc;
+  }
   if (c->rank == root) {
     uint8_t* b = (uint8_t*)malloc(std::max<size_t>(host.size(), 1));
     if (!b) return ZKL_E_OOM;

@@ -57,7 +57,6 @@ void set_row_digest_rule(int rule);
 int row_digest_rule();
 // DIT passes on lazily reduced limbs (default) or the canonical kernel
 void set_ntt_lazy(bool on);
-void set_ntt_mfma(bool on);
 // n Poseidon permutations of 12-element canonical states in place (engine as above)
 void launch_permute(fe* d_states, size_t n, int engine, hipStream_t s);
 struct CeParams;

@@ -1188,9 +1188,12 @@ int zkl_hip_hash_rows(zkl_ctx* c, const void* d_m, uint32_t nc, uint32_t nr, uin
 }
 
 int zkl_hip_set_ntt_mode(int mode) {
-  if (mode < 0 || mode > 2) return ZKL_E_INVALID;
+  if (mode < 0 || mode > 1) return ZKL_E_INVALID;
+  if (g_proofs_in_flight.load() != 0) {  // every pass of a proof must see one kernel form
+    set_err(nullptr, "the NTT mode cannot change while a proof is in flight");
+    return ZKL_E_INVALID;
+  }
   set_ntt_lazy(mode != 0);
-  set_ntt_mfma(mode == 2);
   return 0;
 }
 

@@ -4,7 +4,8 @@ Segments are independent, so ranks (one process per GPU, launched by
 torch.distributed.run) prove disjoint segment sets with no data-path collective.  The one
 exchange is the aggregation hand-off: the step proofs (and the boundary fields inside them)
 go to rank 0 over RCCL point-to-point transfers between the GPUs (zkl_comm_*, xGMI within a
-node).  Control -- the barrier around the timed region, the max-over-ranks elapsed time, the
+node); with one GPU per rank that transport is required (a failure ends the run non-zero), and
+gloo carries the bytes only in same-device rehearsals or with ZKL_COMM=gloo, labelled as such.  Control -- the barrier around the timed region, the max-over-ranks elapsed time, the
 RCCL unique id -- runs on torch.distributed's gloo backend with CPU tensors: the prover owns
 the GPU through its own HIP runtime (runtime note)."""
 import os
@@ -80,18 +81,51 @@ def gather_to_root(obj):
     return out
 
 
-def init_rccl(device):
+def rccl_required():
+    """True when the hand-off must run over RCCL: more than one rank, each on its own GPU
+    (ZKL_BENCH_DEVICE unset) and no explicit ZKL_COMM=gloo.  Same-device rehearsals
+    (ZKL_BENCH_DEVICE pins every rank to one GPU, which RCCL refuses as a duplicate device) and
+    the explicit opt-out keep the gloo transport, labelled as such in the bench line."""
+    _, world, _ = env()
+    return world > 1 and os.environ.get("ZKL_BENCH_DEVICE") is None and os.environ.get("ZKL_COMM", "rccl") != "gloo"
+
+
+def _watchdog(seconds, what):
+    """Ends the process (exit 3) if `what` has not finished within `seconds`: a collective init
+    whose peers failed would otherwise block forever.  Returns the timer; cancel() it after."""
+    import threading
+
+    def fire():
+        import sys
+        print(f"zkl_hip.dist: {what} did not finish within {seconds}s; exiting", file=sys.stderr, flush=True)
+        os._exit(3)
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
+def init_rccl(device, required=None, timeout_s=180.0):
     """The RCCL communicator of this rank (zkl_hip.Comm): rank 0 draws the unique id and the
-    gloo control plane broadcasts it.  Returns (comm or None, error or None); a failure is
-    reported, and collect_step_proofs then uses the gloo path."""
+    gloo control plane broadcasts it.  Returns (comm or None, error or None).  Before the
+    collective ncclCommInitRank every rank reports whether it can enter it, so either all ranks
+    enter or none does; a watchdog ends a rank whose init blocks (a peer failed inside it).
+    When `required` (default: rccl_required()) any failure raises instead of returning the
+    error, so a broken RCCL setup on a multi-GPU node fails the run rather than falling back."""
     global _comm, _comm_error
+    if required is None:
+        required = rccl_required()
     if _comm is not None or _comm_error is not None:
+        if required and _comm is None:
+            raise RuntimeError(f"RCCL hand-off required but unavailable: {_comm_error}")
         return _comm, _comm_error
     import zkl_hip
     rank, world, _ = env()
     err, uid = None, None
     if os.environ.get("ZKL_COMM", "rccl") == "gloo":
         err = "ZKL_COMM=gloo"
+    elif world > 1 and os.environ.get("ZKL_BENCH_DEVICE") is not None:
+        err = "same-device rehearsal (ZKL_BENCH_DEVICE pins every rank to one GPU; RCCL needs one GPU per rank)"
     # every rank must be able to enter ncclCommInitRank, or none does (it is collective)
     avail = gather_to_root(err or zkl_hip.comm_available())
     if rank == 0:
@@ -107,10 +141,14 @@ def init_rccl(device):
     uid, err = box
     comm = None
     if err is None:
+        wd = _watchdog(timeout_s, "ncclCommInitRank") if world > 1 else None
         try:
             comm = zkl_hip.Comm(device, world, rank, uid)
         except Exception as e:  # noqa: BLE001
             err = str(e)
+        finally:
+            if wd is not None:
+                wd.cancel()
     errs = gather_to_root(err) if _dist is not None else [err]
     if _dist is not None:  # every rank takes the same transport
         flag = [next((e for e in (errs or []) if e), None)] if rank == 0 else [None]
@@ -120,6 +158,8 @@ def init_rccl(device):
         comm.close()
         comm = None
     _comm, _comm_error = comm, err
+    if required and comm is None:
+        raise RuntimeError(f"RCCL hand-off required but unavailable: {err}")
     return comm, err
 
 
@@ -145,7 +185,13 @@ def gather_step_bytes(step_bytes, comm=None):
     """Every rank's step encodings on rank 0 (list per rank), None elsewhere: over RCCL when a
     communicator is given, else over gloo (host bytes)."""
     if comm is not None:
-        got = comm.gather_bytes(pack_blobs(step_bytes), root=0)
+        _, world, _ = env()
+        wd = _watchdog(300.0, "the RCCL step-proof gather") if world > 1 else None
+        try:
+            got = comm.gather_bytes(pack_blobs(step_bytes), root=0)
+        finally:
+            if wd is not None:
+                wd.cancel()
         return None if got is None else [unpack_blobs(b) for b in got]
     return gather_to_root(list(step_bytes))
 
