@@ -15,7 +15,7 @@ HIPCC = "/opt/rocm/bin/hipcc"
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 def test_montgomery_helpers(tmp_path):
     build = os.path.join(ROOT, "zk-lisp_amd", "build")
-    objs = [os.path.join(build, f) for f in ("host_hash.o", "air_host.o")]
+    objs = [os.path.join(build, f) for f in ("host_hash.o", "host_poseidon_ifma.o", "air_host.o")]
     if not all(os.path.exists(o) for o in objs):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "zk-lisp_amd")], check=True)
     obj = tmp_path / "mont_check.o"

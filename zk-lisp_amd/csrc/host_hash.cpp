@@ -244,9 +244,29 @@ Hasher::Hasher() {
   dom_many = domain_fe("zkl/winter/hash/merge_many");
   dom_int = domain_fe("zkl/winter/hash/merge_with_int");
   dom_elems = domain_fe("winter/hash/elements");
+  // the vector permutation is used only after it reproduces the scalar one on a few states
+  if (ifma_available()) {
+    IfmaSuite* v = ifma_new();
+    ifma_prepare(suite, *v);
+    bool same = true;
+    for (uint64_t t = 0; t < 4 && same; t++) {
+      fe a[12], b[12];
+      for (int i = 0; i < 12; i++) a[i] = b[i] = fe{0x9E3779B97F4A7C15ull * (t * 12 + i + 1), t ? ~(uint64_t)i >> t : 0};
+      for (int i = 0; i < 12; i++)
+        if (a[i].hi == P_HI && a[i].lo >= P_LO) a[i] = b[i] = fe{a[i].lo, 0};
+      permute_with(suite, a);
+      ifma_permute(*v, b);
+      for (int i = 0; i < 12; i++) same = same && a[i].lo == b[i].lo && a[i].hi == b[i].hi;
+    }
+    if (same) ifma = v;
+    else ifma_delete(v);
+  }
 }
 
-void Hasher::permute(fe st[12]) const { permute_with(suite, st); }
+void Hasher::permute(fe st[12]) const {
+  if (ifma) ifma_permute(*ifma, st);
+  else permute_with(suite, st);
+}
 
 fe Hasher::sponge(fe dom_fe, const fe* m, size_t n) const {
   fe st[12] = {};

@@ -33,8 +33,16 @@ fe be_from_le16(const uint8_t b[16]);
 void program_field_commitment(const uint8_t b32[32], fe out[2]);
 
 // The commitment/coin hasher: suite [0;32], 27 rounds (poseidon/hasher.rs:23,235-241).
+struct IfmaSuite;  // host_poseidon_ifma.cpp
+bool ifma_available();
+void ifma_prepare(const PoseidonSuite& s, IfmaSuite& out);
+void ifma_permute(const IfmaSuite& s, fe st[12]);
+IfmaSuite* ifma_new();
+void ifma_delete(IfmaSuite* p);
+
 struct Hasher {
   PoseidonSuite suite;
+  IfmaSuite* ifma = nullptr;  // the AVX-512 IFMA form of suite when the CPU has it (checked)
   fe dom_bytes, dom_merge, dom_many, dom_int, dom_elems;  // folded domain labels
   Hasher();
   void permute(fe st[12]) const;

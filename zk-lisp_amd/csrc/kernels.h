@@ -65,6 +65,10 @@ void upload_air_consts(ProofConsts* dK, const AirDevice& a, hipStream_t s);
 // transition composition coefficients alpha_j: copied device->device from the draw buffer
 void upload_alphas_from_device(ProofConsts* dK, const fe* d_alphas, int n, hipStream_t s);
 void upload_deep_coeffs(ProofConsts* dK, const fe* h_coeffs, int n, hipStream_t s);
+// The DEEP coefficients straight from the draw buffer (no host round trip): dK->deep,
+// dK->deep_m (limbs of g * 2^156) and dK->deep_sz from the OOD frame d_frame (t(z) [W] | H(z) [C]
+// | t(zg) [W] | H(zg) [C]).  n = W + C <= 256.
+void launch_deep_coeffs(const fe* d_gam, uint32_t W, uint32_t C, const fe* d_frame, ProofConsts* dK, hipStream_t s);
 
 // ---- hashing --------------------------------------------------------------
 // Row digests of a column-major matrix (ld = rows per column) with Winterfell partitioning.
@@ -157,6 +161,7 @@ struct ProofConsts {
   fe alpha[1024];  // transition composition coefficients
   fe deep[512];   // DEEP coefficients (trace then composition columns)
   uint32_t deep_m[512][5];  // the same as 26-bit limbs of g * 2^156 mod p (deep_kernel)
+  fe deep_sz[2];  // sum_i g_i * frame_i(z), sum_i g_i * frame_i(z g) (deep_coeffs_kernel)
 };
 void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab,
                             const fe* d_bm /* (n_bcols + 1) x ce */, const CeParams& p, ProofConsts* dK,
@@ -183,10 +188,14 @@ struct OodArgs {
   uint32_t off[16];
 };
 void launch_ood(const OodArgs& a, fe* d_partial, hipStream_t s);
-struct DeepParams {
+// The OOD frame from the two launch_ood partial sets: chunk sums, composition columns scaled by
+// mult[j]; written in transcript order t(z) [W] | H(z) [C] | t(zg) [W] | H(zg) [C].
+void launch_ood_frame(const fe* d_partial_trace, const fe* d_partial_comp, uint32_t W, uint32_t C, uint32_t chunks,
+                      const fe* mult /* C host values */, fe* d_frame, hipStream_t s);
+struct DeepParams {  // the frame dot products come from ProofConsts::deep_sz (launch_deep_coeffs)
   size_t N;
   uint32_t W, C;
-  fe z, zg, sz, szg;
+  fe z, zg;
 };
 // d_dinv[i] = 1/((x_i - z)(x_i - zg)) over the LDE coset x_i = 3*w_N^i (launch before launch_deep)
 void launch_deep_denoms(const fe* d_roots, size_t Ntab, size_t N, fe z, fe zg, fe* d_dinv, hipStream_t s);

@@ -950,10 +950,71 @@ __global__ __launch_bounds__(256) void deep_kernel(const fe* __restrict__ lde, c
     const size_t i = lde_row(i0 + k * T, p.N, split);
     const fe x = fe_mul(fe{3, 0}, roots[i << shift]);
     const fe d1 = fe_sub(x, p.z), d2 = fe_sub(x, p.zg);
-    const fe num = fe_add(fe_mul(fe_sub(sv, p.sz), d2), fe_mul(fe_sub(sv, p.szg), d1));
+    const fe num = fe_add(fe_mul(fe_sub(sv, K->deep_sz[0]), d2), fe_mul(fe_sub(sv, K->deep_sz[1]), d1));
     out[i] = fe_mul(num, dinv[i]);
   }
 }
+// One block: thread i < W + C stores coefficient i and its Montgomery limbs; both frame dot
+// products are summed by a tree reduction in LDS.
+__global__ __launch_bounds__(256) void deep_coeffs_kernel(const fe* __restrict__ gam, uint32_t W, uint32_t C,
+                                                          const fe* __restrict__ frame, fe R156, ProofConsts* K) {
+  __shared__ fe red[2][256];
+  const uint32_t i = threadIdx.x, n = W + C;
+  fe a = fe_zero(), b = fe_zero();
+  if (i < n) {
+    const fe g = gam[i];
+    K->deep[i] = g;
+    uint32_t l[5];
+    to26(fe_mul(g, R156), l);
+#pragma unroll
+    for (int t = 0; t < 5; t++) K->deep_m[i][t] = l[t];
+    a = fe_mul(g, frame[i]);
+    b = fe_mul(g, frame[n + i]);
+  }
+  red[0][i] = a;
+  red[1][i] = b;
+  __syncthreads();
+  for (uint32_t h = 128; h > 0; h >>= 1) {
+    if (i < h) {
+      red[0][i] = fe_add(red[0][i], red[0][i + h]);
+      red[1][i] = fe_add(red[1][i], red[1][i + h]);
+    }
+    __syncthreads();
+  }
+  if (i == 0) {
+    K->deep_sz[0] = red[0][0];
+    K->deep_sz[1] = red[1][0];
+  }
+}
+void launch_deep_coeffs(const fe* d_gam, uint32_t W, uint32_t C, const fe* d_frame, ProofConsts* dK, hipStream_t s) {
+  if (W + C > 256) throw std::invalid_argument("more than 256 DEEP coefficients (W + C)");
+  deep_coeffs_kernel<<<1, 256, 0, s>>>(d_gam, W, C, d_frame, fe_pow64(fe{2, 0}, 156), dK);
+}
+
+struct OodMult {
+  fe m[16];
+};
+__global__ void ood_frame_kernel(const fe* __restrict__ pt, const fe* __restrict__ pc, uint32_t W, uint32_t C,
+                                 uint32_t chunks, OodMult mult, fe* __restrict__ frame) {
+  const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;  // output slot in transcript order
+  const uint32_t n = W + C;
+  if (o >= 2 * n) return;
+  const uint32_t pt_ = o / n, r = o % n;  // point (z, zg), column in t | H
+  const bool tr = r < W;
+  const fe* src = tr ? pt + ((size_t)pt_ * W + r) * chunks : pc + ((size_t)pt_ * C + (r - W)) * chunks;
+  fe acc = fe_zero();
+  for (uint32_t k = 0; k < chunks; k++) acc = fe_add(acc, src[k]);
+  frame[o] = tr ? acc : fe_mul(acc, mult.m[r - W]);
+}
+void launch_ood_frame(const fe* d_pt, const fe* d_pc, uint32_t W, uint32_t C, uint32_t chunks, const fe* mult,
+                      fe* d_frame, hipStream_t s) {
+  if (C > 16) throw std::invalid_argument("more than 16 composition columns");
+  OodMult m{};
+  for (uint32_t j = 0; j < C; j++) m.m[j] = mult[j];
+  const uint32_t outs = 2 * (W + C);
+  ood_frame_kernel<<<(outs + 127) / 128, 128, 0, s>>>(d_pt, d_pc, W, C, chunks, m, d_frame);
+}
+
 void launch_deep_denoms(const fe* d_roots, size_t Ntab, size_t N, fe z, fe zg, fe* d_dinv, hipStream_t s) {
   launch_coset_inv(d_roots, ilog2s(Ntab) - ilog2s(N), N, z, zg, 1, d_dinv, s);
 }

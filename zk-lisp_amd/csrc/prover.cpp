@@ -92,7 +92,7 @@ struct zkl_ctx {
   size_t tab_n = 0, tab_N = 0;
   DBuf roots, iroots, mroots, miroots, opow, opow_n, pertab;
   // work buffers
-  DBuf trace, coef, lde, parts, tree, ce, bvec, bm, clde, ctree, deep, draws, pw, oodv, asl, ast, asv, ars;
+  DBuf trace, coef, lde, parts, tree, ce, bvec, bm, clde, ctree, deep, draws, pw, oodv, oodf, asl, ast, asv, ars;
   DBuf fri_ev, fri_tree, best, gaddr, gout, flag;
   DBuf xinv;    // batch-inverted coset denominators of DEEP (z-dependent)
   DBuf cexinv;  // 1 / (x - g^(n-1)) over the CE coset: shape-only, kept while the key matches
@@ -656,14 +656,21 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     for (int j = 0; j < Cc; j++) b.off[j] = bitrev_u((uint32_t)j, loge);
     launch_ood(b, dood + n_otr, s);
   }
+  std::vector<fe> cmult(Cc);
+  for (int j = 0; j < Cc; j++) cmult[j] = fe_mul(fe_pow64(inv3, (uint64_t)j * n), inv_ce);
+  // chunk sums and the composition scaling on the device, so only the 2 (W + C) frame values
+  // cross PCIe (a small copy: no SDMA start-up latency in the transcript's critical path)
+  C->oodf.ensure(2 * ((size_t)W + Cc) * sizeof(fe));
+  fe* dframe = C->oodf.f();
+  launch_ood_frame(dood, dood + n_otr, W, (uint32_t)Cc, chunks, cmult.data(), dframe, s);
   check_launch("OOD evaluation");
-  std::vector<fe> hood(2 * ((size_t)W + Cc), fe_zero());
-  C->h_ood.ensure((n_otr + n_ocp) * sizeof(fe));
-  const fe* part = C->h_ood.at<fe>();
-  HIPCHECK(hipMemcpyAsync(C->h_ood.p, dood, (n_otr + n_ocp) * sizeof(fe), hipMemcpyDeviceToHost, s));
+  const size_t nfr = 2 * ((size_t)W + Cc);
+  C->h_ood.ensure(nfr * sizeof(fe));
+  const fe* frame = C->h_ood.at<fe>();
+  HIPCHECK(hipMemcpyAsync(C->h_ood.p, dframe, nfr * sizeof(fe), hipMemcpyDeviceToHost, s));
   HIPCHECK(hipEventRecord(C->hev, s));
-  // the DEEP denominators depend on z only: the device computes them while the host sums the
-  // OOD partials and hashes them into the transcript
+  // the DEEP denominators depend on z only: the device computes them while the host hashes the
+  // frame into the transcript
   C->xinv.ensure(std::max(ce, N) * sizeof(fe));
   {
     KScope k(C, KF_DEEP);
@@ -672,44 +679,23 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   check_launch("DEEP denominators");
   HT("ood_enqueued");
   HIPCHECK(hipEventSynchronize(C->hev));
-  // hood = t(z) [W] | t(zg) [W] | chat(z) [Cc] | chat(zg) [Cc]
-  for (size_t pt = 0; pt < 2; pt++) {
-    for (uint32_t c = 0; c < W; c++)
-      for (uint32_t k = 0; k < chunks; k++)
-        hood[pt * W + c] = fe_add(hood[pt * W + c], part[(pt * W + c) * chunks + k]);
-    for (int j = 0; j < Cc; j++)
-      for (uint32_t k = 0; k < chunks; k++)
-        hood[2 * W + pt * Cc + j] = fe_add(hood[2 * W + pt * Cc + j], part[n_otr + (pt * Cc + j) * chunks + k]);
-  }
-  std::vector<fe> tz(hood.begin(), hood.begin() + W), tzg(hood.begin() + W, hood.begin() + 2 * W);
-  std::vector<fe> hz(Cc), hzg(Cc);
-  for (int j = 0; j < Cc; j++) {
-    fe mult = fe_mul(fe_pow64(inv3, (uint64_t)j * n), inv_ce);
-    hz[j] = fe_mul(hood[2 * W + j], mult);
-    hzg[j] = fe_mul(hood[2 * W + Cc + j], mult);
-  }
-  std::vector<fe> oodcat;
-  oodcat.insert(oodcat.end(), tz.begin(), tz.end());
-  oodcat.insert(oodcat.end(), hz.begin(), hz.end());
-  oodcat.insert(oodcat.end(), tzg.begin(), tzg.end());
-  oodcat.insert(oodcat.end(), hzg.begin(), hzg.end());
-  coin.reseed(H.hash_elements(oodcat.data(), oodcat.size()));
+  // frame = t(z) [W] | H(z) [Cc] | t(zg) [W] | H(zg) [Cc]: the order hashed (agg/fs.rs:152-164)
+  std::vector<fe> tz(frame, frame + W), hz(frame + W, frame + W + Cc);
+  std::vector<fe> tzg(frame + W + Cc, frame + 2 * W + Cc), hzg(frame + 2 * W + Cc, frame + nfr);
+  coin.reseed(H.hash_elements(frame, nfr));
   T.mark(5);
 
-  // ---- 5. DEEP composition coefficients (W trace, then C constraint) and evaluations
+  // ---- 5. DEEP composition coefficients (W trace, then C constraint) and evaluations: drawn,
+  // converted and dotted with the frame on the device
   HT("ood_hashed");
-  std::vector<fe> gam(W + Cc);
   launch_draws(coin.seed, coin.counter, W + Cc, C->draws.f(), s);
   check_launch("DEEP coefficient draws");
   coin.counter += W + Cc;
-  d2h(C, gam.data(), C->draws.p, gam.size() * sizeof(fe));
+  launch_deep_coeffs(C->draws.f(), W, (uint32_t)Cc, dframe, dK, s);
+  check_launch("DEEP coefficients");
   HT("gam");
-  upload_deep_coeffs(dK, gam.data(), (int)gam.size(), s);
   DeepParams dp{};
   dp.N = N; dp.W = W; dp.C = Cc; dp.z = z; dp.zg = zg;
-  dp.sz = fe_zero(); dp.szg = fe_zero();
-  for (uint32_t c = 0; c < W; c++) { dp.sz = fe_add(dp.sz, fe_mul(gam[c], tz[c])); dp.szg = fe_add(dp.szg, fe_mul(gam[c], tzg[c])); }
-  for (int j = 0; j < Cc; j++) { dp.sz = fe_add(dp.sz, fe_mul(gam[W + j], hz[j])); dp.szg = fe_add(dp.szg, fe_mul(gam[W + j], hzg[j])); }
   C->deep.ensure(N * sizeof(fe));
   {
     KScope k(C, KF_DEEP);
@@ -755,16 +741,16 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   }
   check_launch("FRI layers");
   HT("fri_enqueued");
+  size_t Nr = N >> nl;
+  std::vector<fe> rem_ev(Nr), cs(2 + (size_t)nl);
+  // the layer coins / roots and the remainder evaluations in one round trip
+  if (nl > 0) HIPCHECK(hipMemcpyAsync(cs.data(), d_coin, cs.size() * sizeof(fe), hipMemcpyDeviceToHost, s));
+  d2h(C, rem_ev.data(), layer_ev(nl), Nr * sizeof(fe));
   if (nl > 0) {
-    std::vector<fe> cs(2 + (size_t)nl);
-    d2h(C, cs.data(), d_coin, cs.size() * sizeof(fe));
     for (int d = 0; d < nl; d++) fri_roots[d] = cs[2 + d];
     coin.seed = cs[0];
     coin.counter = 1;
   }
-  size_t Nr = N >> nl;
-  std::vector<fe> rem_ev(Nr);
-  d2h(C, rem_ev.data(), layer_ev(nl), Nr * sizeof(fe));
   // interpolate over 3*<w_Nr> (constant domain offset, agg/trace.rs:940-952), keep rem_deg+1, reversed
   std::vector<fe> rc(Nr);
   {
@@ -834,6 +820,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   HT("q_sorted");
   // gather plan: trace rows, comp rows, trace/comp tree nodes, FRI values + tree nodes
   std::vector<uint64_t> addrs;
+  addrs.reserve(nq * ((size_t)W + Cc) + 2 * nq * (size_t)(logN + 2) * (nl + 2) + 64);
   auto A = [&](const fe* p) { addrs.push_back((uint64_t)(uintptr_t)p); };
   for (size_t k = 0; k < nq; k++)
     for (uint32_t c = 0; c < W; c++) A(C->lde.f() + (size_t)c * N + lde_pos(pos[k], N, split));
@@ -876,6 +863,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
 
   // ---- 9. Proof::to_bytes  [WF-recall layout, DESIGN.md §Proof bytes]
   Bytes P;
+  P.v.reserve(na_g * 32 + 4096);
   P.u8((uint8_t)W); P.u8(0); P.u8(0); P.u8((uint8_t)logn); P.u8(0); P.u8(0);  // TraceInfo
   P.u8(16); P.felem(fe{P_LO, P_HI});                                           // modulus bytes
   P.u8((uint8_t)o.num_queries); P.u8((uint8_t)o.blowup_factor); P.u8((uint8_t)o.grinding_factor);
@@ -899,8 +887,10 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     }
   };
   Bytes tv, cv, tp, cpb;
-  for (size_t k = 0; k < nq * W; k++) tv.felem(gv[gi++]);
-  for (size_t k = 0; k < nq * Cc; k++) cv.felem(gv[gi++]);
+  tv.raw(gv + gi, nq * W * sizeof(fe));  // felem = the 16 LE bytes of the canonical value
+  gi += nq * W;
+  cv.raw(gv + gi, nq * Cc * sizeof(fe));
+  gi += nq * Cc;
   emit_multiproof(tp, tplan, logN);
   emit_multiproof(cpb, tplan, logN);
   P.usize(1);
