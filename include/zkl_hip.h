@@ -365,7 +365,10 @@ typedef struct {
  *   last-row assertions of agg/air.rs:276-304 can hold) and zero root-error columns (every
  *   opening was verified against its root under the library's row-digest rule); the batch must
  *   satisfy ZlAggAir, otherwise ZKL_E_INVALID.  This is what zkl_agg_prove writes to proof.bin.
- * ZKL_AGG_TRACE_REFERENCE: the trace agg/trace.rs:397-398,553-690 builds, byte for byte:
+ * ZKL_AGG_TRACE_REFERENCE: the trace agg/trace.rs:397-398,553-690 builds -- PARITY UNPINNED:
+ *   checked only against the Python restatement oracle/agg_ref.py (no fixture from the reference
+ *   exists; its batch-proof decompression order and partition_size are [WF-recall] rules), so
+ *   "the reference's trace" means "the restatement of agg/trace.rs", not bytes seen from it:
  *   next_pow2(max(children, 8)) rows and root-error columns sum_k(root_k - root) where root_k is
  *   reproduced from the opening's row under hash_row_poseidon (agg/child.rs:1025-1045, one chunk
  *   not merged).  No AIR check, like the reference's release prover: for a power-of-two child

@@ -98,6 +98,8 @@ def test_check_request_accepts_valid():
     (dict(field_extension=2), "FieldExtension::None"),
     (dict(fri_folding_factor=4), "folding factor"),
     (dict(fri_remainder_max_degree=2), "fri_remainder_max_degree"),
+    # the verifier's bound (remainder degree below the blowup) holds in the prover too
+    (dict(blowup_factor=8, fri_remainder_max_degree=15), "below the blowup factor"),
     (dict(batching_constraints=1), "Linear"),
     (dict(batching_deep=1), "Linear"),
     (dict(num_partitions=0), "num_partitions"),

@@ -525,7 +525,7 @@ def test_lde_lazy_ntt_matches_canonical(gpu_ctx, ncols, log_n, blow):
     gpu_ctx.upload(d_v, raw, len(raw))
     outs = []
     try:
-        for lazy in (0, 1, 2):
+        for lazy in (0, 1):
             assert lib.zkl_hip_set_ntt_mode(lazy) == 0
             gpu_ctx.lde(d_v, ncols, n, blow, d_c, d_l)
             outs.append(gpu_ctx.download(d_l, 16 * ncols * N))
@@ -533,7 +533,7 @@ def test_lde_lazy_ntt_matches_canonical(gpu_ctx, ncols, log_n, blow):
         lib.zkl_hip_set_ntt_mode(1)
         for d in (d_v, d_c, d_l):
             gpu_ctx.free(d)
-    assert outs[0] == outs[1] == outs[2]
+    assert outs[0] == outs[1]
 
 
 def test_full_size_proof_independent_of_kernel_forms(gpu_ctx):
@@ -548,8 +548,7 @@ def test_full_size_proof_independent_of_kernel_forms(gpu_ctx):
     proofs = {}
     try:
         for name, engine, min_items, lazy in (("default", 1, 1 << 14, 1), ("lane", 0, 1 << 14, 1),
-                                              ("all_mfma", 1, 32, 1), ("canonical_ntt", 1, 1 << 14, 0),
-                                              ("mfma_ntt", 1, 1 << 14, 2)):
+                                              ("all_mfma", 1, 32, 1), ("canonical_ntt", 1, 1 << 14, 0)):
             assert lib.zkl_hip_set_hash_policy(engine, min_items) == 0
             assert lib.zkl_hip_set_ntt_mode(lazy) == 0
             proofs[name] = gpu_ctx.prove_segment(t, w, n, pi, opts)
@@ -850,3 +849,24 @@ def test_split_lde_layout_proofs_match_oracle(oracle, gpu_ctx, flags, blowup):
     ot, opi, _ = oracle.synth_segment(seed, 8, flags)
     want = oracle.prove(ot, w, n, opi, oracle.ProofOptions(*[getattr(opts, f) for f, _ in opts._fields_]))
     assert got == want
+
+
+def test_remainder_degree_boundary_prove_then_verify(oracle, gpu_ctx):
+    """the largest remainder degree the verifier accepts at a blowup (7 at blowup 8)
+    proves, equals the oracle's proof and verifies with the product verifier; one step further
+    (15) is refused by the prover as by the verifier."""
+    import zkl_hip
+    log_n = 8
+    n = 1 << log_n
+    trace, pi, w = zkl_hip.synth_vm_segment(0x5EED0B08, log_n)
+    opts = zkl_hip.proof_options(w, n, queries=16, blowup=8, grind=4)
+    opts.fri_remainder_max_degree = 7
+    got = gpu_ctx.prove_segment(trace, w, n, pi, opts)
+    ot, opi, _ = oracle.synth_segment(0x5EED0B08, log_n)
+    want = oracle.prove(ot, w, n, opi, oracle.ProofOptions(*[getattr(opts, f) for f, _ in opts._fields_]))
+    assert got == want
+    zkl_hip.verify_segment(got, pi, opts)
+    opts.fri_remainder_max_degree = 15
+    with pytest.raises(zkl_hip.ZklError, match="below the blowup factor"):
+        gpu_ctx.prove_segment(trace, w, n, pi, opts)
+

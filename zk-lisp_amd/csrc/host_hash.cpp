@@ -3,6 +3,7 @@
 // zk-lisp-proof-winterfell/src/poseidon/{mod.rs:56-217,421-440, hasher.rs:57-231}.
 #include "host_hash.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <array>
@@ -245,7 +246,8 @@ Hasher::Hasher() {
   dom_int = domain_fe("zkl/winter/hash/merge_with_int");
   dom_elems = domain_fe("winter/hash/elements");
   // the vector permutation is used only after it reproduces the scalar one on a few states
-  if (ifma_available()) {
+  const char* env = getenv("ZKL_HOST_IFMA");  // ZKL_HOST_IFMA=0: the scalar permutation (A/B)
+  if (ifma_available() && !(env && !strcmp(env, "0"))) {
     IfmaSuite* v = ifma_new();
     ifma_prepare(suite, *v);
     bool same = true;

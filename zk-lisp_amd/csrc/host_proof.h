@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <vector>
 
 #include "field.h"
@@ -63,35 +64,48 @@ struct Plan {
 };
 inline Plan batch_plan(size_t n_leaves, const std::vector<size_t>& idx) {
   const int depth = ilog2(n_leaves);
-  std::vector<size_t> norm(idx.size()), req(idx);
-  for (size_t k = 0; k < idx.size(); k++) norm[k] = idx[k] & ~(size_t)1;
-  std::sort(norm.begin(), norm.end());
-  norm.erase(std::unique(norm.begin(), norm.end()), norm.end());
-  std::sort(req.begin(), req.end());
+  const size_t Q = idx.size();
+  // normalised leaf pairs (sorted, unique) and the requested leaves (sorted) in one scratch block
+  std::unique_ptr<size_t[]> buf(new size_t[2 * Q + 2]);
+  size_t* norm = buf.get();
+  size_t* req = norm + Q + 1;
+  for (size_t k = 0; k < Q; k++) { norm[k] = idx[k] & ~(size_t)1; req[k] = idx[k]; }
+  std::sort(norm, norm + Q);
+  const size_t L = (size_t)(std::unique(norm, norm + Q) - norm);
+  std::sort(req, req + Q);
   // list k takes at most two leaves and one node per level: fixed-stride scratch, compacted
-  const size_t L = norm.size(), stride = (size_t)depth + 2;
-  std::vector<uint64_t> tmp(L * stride);
-  std::vector<uint32_t> cnt(L, 0);
-  std::vector<size_t> cur(L), next;
-  next.reserve(L);
+  const size_t stride = (size_t)depth + 2;
+  std::unique_ptr<uint64_t[]> tmp(new uint64_t[L * stride]);
+  std::unique_ptr<uint32_t[]> cnt(new uint32_t[L]());
+  std::unique_ptr<size_t[]> cur_b(new size_t[2 * L + 2]);
+  size_t *cur = cur_b.get(), *nxt = cur + L + 1;
   for (size_t k = 0; k < L; k++) {
     for (size_t j = norm[k]; j < norm[k] + 2; j++)
-      if (!std::binary_search(req.begin(), req.end(), j)) tmp[k * stride + cnt[k]++] = n_leaves + j;
+      if (!std::binary_search(req, req + Q, j)) tmp[k * stride + cnt[k]++] = n_leaves + j;
     cur[k] = (norm[k] + n_leaves) >> 1;
   }
+  size_t nc = L;
   for (int lvl = 1; lvl < depth; lvl++) {
-    next.clear();
-    for (size_t i = 0; i < cur.size(); i++) {
-      size_t sib = cur[i] ^ 1;
-      if (i + 1 < cur.size() && cur[i + 1] == sib) i++;
+    size_t nn = 0;
+    for (size_t i = 0; i < nc; i++) {
+      const size_t sib = cur[i] ^ 1;
+      if (i + 1 < nc && cur[i + 1] == sib) i++;
       else tmp[i * stride + cnt[i]++] = sib;
-      next.push_back(sib >> 1);
+      nxt[nn++] = sib >> 1;
     }
-    cur.swap(next);
+    std::swap(cur, nxt);
+    nc = nn;
   }
   Plan P;
-  P.len = cnt;
-  for (size_t k = 0; k < L; k++) P.node.insert(P.node.end(), tmp.begin() + k * stride, tmp.begin() + k * stride + cnt[k]);
+  P.len.assign(cnt.get(), cnt.get() + L);
+  size_t tot = 0;
+  for (size_t k = 0; k < L; k++) tot += cnt[k];
+  P.node.resize(tot);
+  size_t o = 0;
+  for (size_t k = 0; k < L; k++) {
+    memcpy(P.node.data() + o, tmp.get() + k * stride, cnt[k] * sizeof(uint64_t));
+    o += cnt[k];
+  }
   return P;
 }
 

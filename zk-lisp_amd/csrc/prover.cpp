@@ -296,6 +296,13 @@ void validate_request(uint32_t W, uint32_t n32, const zkl_air_public_inputs& pi,
   if (o.hash_rate < 1 || o.hash_rate > 255) throw InvalidArg("hash_rate must be in 1..255 (a u8 in the proof context)");
   if (o.fri_remainder_max_degree > 15 || ((o.fri_remainder_max_degree + 1) & o.fri_remainder_max_degree))
     throw InvalidArg("fri_remainder_max_degree must be one less than a power of two, at most 15");
+  // the bounds the verifier applies to the options it decodes from the proof (verifier.cpp): a
+  // request the library's own verifier, and the aggregation's child replay, would reject is
+  // refused here rather than proved (remainder degree >= blowup)
+  {
+    const std::string e = check_proof_options(o);
+    if (!e.empty()) throw InvalidArg(e);
+  }
   if (pi.n_main_slots > ZKL_MAX_MAIN_SLOTS) throw InvalidArg("n_main_slots exceeds ZKL_MAX_MAIN_SLOTS");
   if (W == 0 || W > 4096) throw InvalidArg("trace width must be in 1..4096");
 }
@@ -427,12 +434,16 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->lde.ensure((size_t)W * N * sizeof(fe));
   // columns [c0, c0 + nc): iNTT -> n*coef bit-reversed, scale c_k * 3^k (coset shift), DIT
   // every chunk takes the same pass split, so all columns share one layout
-  int split = 0;
+  int split = -1;
   auto lde_cols = [&](uint32_t c0, uint32_t nc) {
     fe* cf = C->coef.f() + (size_t)c0 * n;
     launch_ntt_stages(cf, nc, n, true, 0, logn - 1, miroots, Ntab, s);
     launch_scale_bitrev(cf, nc, n, C->opow_n.f(), s);
-    split = launch_lde_from_coeffs(cf, nc, n, N, mroots, Ntab, C->lde.f() + (size_t)c0 * N, s, g_lde_split);
+    const int sp = launch_lde_from_coeffs(cf, nc, n, N, mroots, Ntab, C->lde.f() + (size_t)c0 * N, s, g_lde_split);
+    // the row hash, evaluator and DEEP read every column with one layout (the NTT mode cannot
+    // change during a proof: zkl_hip_set_ntt_mode refuses while one is in flight)
+    if (split >= 0 && sp != split) throw std::runtime_error("internal: trace LDE chunks in different layouts");
+    split = sp;
   };
   if (trace_on_host) {
     KScope k(C, KF_NTT);
@@ -444,6 +455,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     lde_cols(0, W);
   }
   check_launch("trace LDE");
+  if (split < 0) split = 0;
   T.mark(1);
   // ---- trace commitment (commit_to_rows + MerkleTree)
   C->parts.ensure((size_t)o.num_partitions * N * sizeof(fe) + N * sizeof(fe));
@@ -923,8 +935,10 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   T.mark(9);
   T.mark(10);
   T.finish();
+  HT("stage_events");
   resolve_kernel_times(C);
   out.swap(P.v);
+  HT("returned");
   C->host_ms[2] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call0).count();
   {
     float gpu_ms = 0;
