@@ -126,6 +126,9 @@ void zkl_hip_destroy(zkl_ctx* ctx);
 const char* zkl_hip_last_error(const zkl_ctx* ctx); /* ctx may be NULL */
 void zkl_hip_free(uint8_t* buf);
 int zkl_hip_abi_version(void);
+/* compiled-in tuning values of the kernels ("NAME=value;..."): every value is a supported,
+ * parity-tested configuration (no timing probes are compiled in; tests/test_abi.py) */
+const char* zkl_hip_build_config(void);
 
 /* ---- the drop-in: one segment proof ----------------------------------------
  * Replaces ZkProver::prove -> winterfell::Prover::prove (prove.rs:174-257) for

@@ -30,6 +30,18 @@ def test_abi_version():
     assert zkl_hip.load_library().zkl_hip_abi_version() == 1
 
 
+def test_build_carries_only_default_tuning_values():
+    """VERDICT r3 next 6: no timing probe or losing variant is compiled into the shipped library;
+    the Poseidon translation unit is built with the max-ilp scheduler."""
+    import zkl_hip
+    lib = zkl_hip.load_library()
+    lib.zkl_hip_build_config.restype = C.c_char_p
+    cfg = dict(kv.split("=") for kv in lib.zkl_hip_build_config().decode().split(";"))
+    assert cfg == {"PM_WAVES": "8", "PM_WIDE": "0", "PM_ROW_WAVES": "8", "PM_IGLP": "0", "TAIL_PRIO": "0",
+                   "PW_MAX_ITEMS": "2048", "PM_ROW_BIG": "0", "POSEIDON_SCHED": "max-ilp", "NTT_ELEMS": "1024",
+                   "NTT_THREADS": "256", "CE_WAVES": "3", "DEEP_PTS": "2", "DEEP_COLS": "4"}
+
+
 def test_select_partitions():
     import zkl_hip
     for w, n, exp in [(204, 1 << 12, (1, 16)), (204, 1 << 14, (2, 16)), (204, 1 << 16, (4, 16)),

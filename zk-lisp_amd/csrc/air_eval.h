@@ -90,20 +90,21 @@ __host__ __device__ __forceinline__ fe air_transition_sum(const AirDevice& c_air
 #pragma unroll
       for (int t = 0; t < 5; t++) A.emit(fe_add_sel(fe_mul(p_map, fe_mul(v[t], fe_sub_sel(v[t], one))), s_high));
     }
-    fe bo[17];
-#pragma unroll
-    for (int k = 0; k < 17; k++) bo[k] = cur(C.op[k]);
+    // op bits read through cur() wherever used: a local fe[17] indexed in the loops below was
+    // placed in scratch (288 B per lane), and a kernel that needs scratch makes the runtime
+    // allocate the queue's scratch memory on a later dispatch
+    auto bo = [&](int k) { return cur(C.op[k]); };
     enum { CONST, MOV, ADD, SUB, MUL, NEG, EQ, SEL, SPONGE, ASSERT, ABIT, ARANGE, DIVMOD, DIV128, MULWIDE, LOAD, STORE };
-    fe uses_a = fe_add_sel(fe_add_sel(fe_add_sel(bo[MOV], bo[ADD]), fe_add_sel(bo[SUB], bo[MUL])), fe_add_sel(fe_add_sel(bo[NEG], bo[EQ]), bo[SEL]));
-    uses_a = fe_add_sel(uses_a, fe_add_sel(fe_add_sel(bo[DIVMOD], bo[DIV128]), fe_add_sel(fe_add_sel(bo[MULWIDE], bo[LOAD]), bo[STORE])));
-    fe uses_b = fe_add_sel(fe_add_sel(fe_add_sel(bo[ADD], bo[SUB]), fe_add_sel(bo[MUL], bo[EQ])), fe_add_sel(bo[SEL], bo[DIVMOD]));
-    uses_b = fe_add_sel(uses_b, fe_add_sel(fe_add_sel(bo[DIV128], bo[MULWIDE]), bo[STORE]));
-    fe uses_c = fe_add_sel(fe_add_sel(bo[SEL], bo[ASSERT]), fe_add_sel(bo[ABIT], bo[ARANGE]));
+    fe uses_a = fe_add_sel(fe_add_sel(fe_add_sel(bo(MOV), bo(ADD)), fe_add_sel(bo(SUB), bo(MUL))), fe_add_sel(fe_add_sel(bo(NEG), bo(EQ)), bo(SEL)));
+    uses_a = fe_add_sel(uses_a, fe_add_sel(fe_add_sel(bo(DIVMOD), bo(DIV128)), fe_add_sel(fe_add_sel(bo(MULWIDE), bo(LOAD)), bo(STORE))));
+    fe uses_b = fe_add_sel(fe_add_sel(fe_add_sel(bo(ADD), bo(SUB)), fe_add_sel(bo(MUL), bo(EQ))), fe_add_sel(bo(SEL), bo(DIVMOD)));
+    uses_b = fe_add_sel(uses_b, fe_add_sel(fe_add_sel(bo(DIV128), bo(MULWIDE)), bo(STORE)));
+    fe uses_c = fe_add_sel(fe_add_sel(bo(SEL), bo(ASSERT)), fe_add_sel(bo(ABIT), bo(ARANGE)));
     fe op_any = fe_zero();
 #pragma unroll
-    for (int k = 0; k <= MULWIDE; k++) op_any = fe_add_sel(op_any, bo[k]);
-    fe uses_d0 = fe_add_sel(fe_sub_sel(op_any, bo[SPONGE]), bo[LOAD]);
-    fe uses_d1 = fe_add_sel(fe_add_sel(bo[DIVMOD], bo[DIV128]), bo[MULWIDE]);
+    for (int k = 0; k <= MULWIDE; k++) op_any = fe_add_sel(op_any, bo(k));
+    fe uses_d0 = fe_add_sel(fe_sub_sel(op_any, bo(SPONGE)), bo(LOAD));
+    fe uses_d1 = fe_add_sel(fe_add_sel(bo(DIVMOD), bo(DIV128)), bo(MULWIDE));
     A.emit(fe_add_sel(fe_mul(p_map, fe_sub_sel(sum_d0, uses_d0)), s_low));
     A.emit(fe_add_sel(fe_mul(p_map, fe_sub_sel(sum_a, uses_a)), s_low));
     A.emit(fe_add_sel(fe_mul(p_map, fe_sub_sel(sum_b, uses_b)), s_low));
@@ -125,13 +126,13 @@ __host__ __device__ __forceinline__ fe air_transition_sum(const AirDevice& c_air
     fe op_sum = fe_zero();
 #pragma unroll
     for (int k = 0; k < 17; k++) {
-      A.emit(fe_add_sel(fe_mul(p_map, fe_mul(bo[k], fe_sub_sel(bo[k], one))), s_high));
-      op_sum = fe_add_sel(op_sum, bo[k]);
+      A.emit(fe_add_sel(fe_mul(p_map, fe_mul(bo(k), fe_sub_sel(bo(k), one))), s_high));
+      op_sum = fe_add_sel(op_sum, bo(k));
     }
     A.emit(fe_add_sel(fe_mul(p_map, fe_mul(op_sum, fe_sub_sel(op_sum, one))), s_high));
 #pragma unroll
     for (int k = 0; k < 17; k++)
-      A.emit(fe_add_sel(fe_mul(rom_on, fe_mul(p_map, fe_sub_sel(bo[k], cur(C.rom_op_start + k)))), s_high));
+      A.emit(fe_add_sel(fe_mul(rom_on, fe_mul(p_map, fe_sub_sel(bo(k), cur(C.rom_op_start + k)))), s_high));
     fe pc_c = cur(C.pc), pc_n = nxt(C.pc);
     A.emit(fe_add_sel(fe_mul(rom_on, fe_mul(g_carry, fe_sub_sel(pc_n, pc_c))), s_low));
     A.emit(fe_add_sel(fe_mul(rom_on, fe_mul(p_pad_last, fe_sub_sel(pc_n, fe_add_sel(pc_c, one)))), s_low));
@@ -156,26 +157,26 @@ __host__ __device__ __forceinline__ fe air_transition_sum(const AirDevice& c_air
       A.emit(fe_add_sel(fe_mul(g_carry, fe_sub_sel(nxt(C.r_start + r), cur(C.r_start + r))), s_low));
     fe imm = cur(C.imm);
     fe mode64 = cur(C.eq_inv);
-    fe res = fe_mul(bo[CONST], imm);
-    res = fe_add_sel(res, fe_mul(bo[MOV], a_val));
-    res = fe_add_sel(res, fe_mul(bo[ADD], fe_add_sel(a_val, b_val)));
-    res = fe_add_sel(res, fe_mul(bo[SUB], fe_sub_sel(a_val, b_val)));
-    res = fe_add_sel(res, fe_mul(bo[MUL], fe_mul(a_val, b_val)));
-    res = fe_add_sel(res, fe_mul(bo[NEG], fe_neg(a_val)));
-    res = fe_add_sel(res, fe_mul(bo[SEL], fe_add_sel(fe_mul(c_val, a_val), fe_mul(fe_sub_sel(one, c_val), b_val))));
-    res = fe_add_sel(res, fe_mul(bo[SPONGE], cur(C.lanes_start)));
-    if (use_eq) res = fe_add_sel(res, fe_mul(bo[EQ], d0n));
-    if (use_assert) res = fe_add_sel(res, bo[ASSERT]);
-    if (use_abit) res = fe_add_sel(res, bo[ABIT]);
-    res = fe_add_sel(res, fe_mul(bo[LOAD], imm));
+    fe res = fe_mul(bo(CONST), imm);
+    res = fe_add_sel(res, fe_mul(bo(MOV), a_val));
+    res = fe_add_sel(res, fe_mul(bo(ADD), fe_add_sel(a_val, b_val)));
+    res = fe_add_sel(res, fe_mul(bo(SUB), fe_sub_sel(a_val, b_val)));
+    res = fe_add_sel(res, fe_mul(bo(MUL), fe_mul(a_val, b_val)));
+    res = fe_add_sel(res, fe_mul(bo(NEG), fe_neg(a_val)));
+    res = fe_add_sel(res, fe_mul(bo(SEL), fe_add_sel(fe_mul(c_val, a_val), fe_mul(fe_sub_sel(one, c_val), b_val))));
+    res = fe_add_sel(res, fe_mul(bo(SPONGE), cur(C.lanes_start)));
+    if (use_eq) res = fe_add_sel(res, fe_mul(bo(EQ), d0n));
+    if (use_assert) res = fe_add_sel(res, bo(ASSERT));
+    if (use_abit) res = fe_add_sel(res, bo(ABIT));
+    res = fe_add_sel(res, fe_mul(bo(LOAD), imm));
     fe bsum = fe_zero();
     if (use_arange) {
       fe pow2 = one;
       for (int k = 0; k < 32; k++) { bsum = fe_add_sel(bsum, fe_mul(pow2, cur(C.gadget_b + k))); pow2 = fe_add_sel(pow2, pow2); }
-      res = fe_add_sel(res, fe_mul(bo[ARANGE], fe_add_sel(fe_mul(fe_sub_sel(one, imm), bsum), imm)));
+      res = fe_add_sel(res, fe_mul(bo(ARANGE), fe_add_sel(fe_mul(fe_sub_sel(one, imm), bsum), imm)));
     }
     bool uses_two = use_divmod || use_mulwide || use_div128;
-    fe b_two = uses_two ? fe_add_sel(fe_add_sel(bo[DIVMOD], bo[MULWIDE]), bo[DIV128]) : fe_zero();
+    fe b_two = uses_two ? fe_add_sel(fe_add_sel(bo(DIVMOD), bo(MULWIDE)), bo(DIV128)) : fe_zero();
     fe w0 = fe_add_sel(fe_mul(fe_sub_sel(one, b_two), res), fe_mul(b_two, d0n));
     fe w1 = fe_mul(b_two, d1n);
     for (int r = 0; r < 8; r++) {
@@ -187,34 +188,34 @@ __host__ __device__ __forceinline__ fe air_transition_sum(const AirDevice& c_air
     fe diff = fe_sub_sel(a_val, b_val);
     fe inv = cur(C.eq_inv);
     if (use_eq) {
-      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[EQ], fe_mul(d0n, diff))), s_eq));
-      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[EQ], fe_sub_sel(fe_sub_sel(one, d0n), fe_mul(diff, inv)))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo(EQ), fe_mul(d0n, diff))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo(EQ), fe_sub_sel(fe_sub_sel(one, d0n), fe_mul(diff, inv)))), s_eq));
     }
     if (use_divmod) {
-      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[DIVMOD], fe_sub_sel(fe_sub_sel(a_val, fe_mul(b_val, d0n)), d1n))), s_eq));
-      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[DIVMOD], fe_sub_sel(fe_mul(b_val, inv), one))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo(DIVMOD), fe_sub_sel(fe_sub_sel(a_val, fe_mul(b_val, d0n)), d1n))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo(DIVMOD), fe_sub_sel(fe_mul(b_val, inv), one))), s_eq));
     }
     const fe p264 = fe{0, 1};
     if (use_mulwide)
-      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[MULWIDE], fe_sub_sel(fe_mul(a_val, b_val), fe_add_sel(d0n, fe_mul(d1n, p264))))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo(MULWIDE), fe_sub_sel(fe_mul(a_val, b_val), fe_add_sel(d0n, fe_mul(d1n, p264))))), s_eq));
     if (use_div128) {
       fe num128 = fe_add_sel(fe_mul(a_val, p264), imm);
-      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[DIV128], fe_sub_sel(num128, fe_add_sel(fe_mul(b_val, d0n), d1n)))), s_eq));
-      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[DIV128], fe_sub_sel(fe_mul(b_val, inv), one))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo(DIV128), fe_sub_sel(num128, fe_add_sel(fe_mul(b_val, d0n), d1n)))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo(DIV128), fe_sub_sel(fe_mul(b_val, inv), one))), s_eq));
     }
     if (use_assert)
-      A.emit(fe_add_sel(fe_mul(p_final, fe_add_sel(fe_mul(bo[ASSERT], fe_sub_sel(c_val, one)), fe_mul(bo[SEL], fe_mul(c_val, fe_sub_sel(c_val, one))))), s_eq));
-    if (use_abit) A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[ABIT], fe_mul(c_val, fe_sub_sel(c_val, one)))), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_add_sel(fe_mul(bo(ASSERT), fe_sub_sel(c_val, one)), fe_mul(bo(SEL), fe_mul(c_val, fe_sub_sel(c_val, one))))), s_eq));
+    if (use_abit) A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo(ABIT), fe_mul(c_val, fe_sub_sel(c_val, one)))), s_eq));
     if (use_arange) {
       for (int k = 0; k < 32; k++) {
         fe bi = cur(C.gadget_b + k);
-        A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[ARANGE], fe_mul(bi, fe_sub_sel(bi, one)))), s_eq));
+        A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo(ARANGE), fe_mul(bi, fe_sub_sel(bi, one)))), s_eq));
       }
       const fe p232 = fe{1ull << 32, 0};
       fe eq32 = fe_sub_sel(c_val, bsum);
       fe eq64 = fe_sub_sel(c_val, fe_add_sel(d0c, fe_mul(bsum, p232)));
       fe eqt = fe_mul(imm, fe_add_sel(fe_mul(mode64, eq64), fe_mul(fe_sub_sel(one, mode64), eq32)));
-      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo[ARANGE], eqt)), s_eq));
+      A.emit(fe_add_sel(fe_mul(p_final, fe_mul(bo(ARANGE), eqt)), s_eq));
     }
   }
   if (RM && c_air.ram_block) {

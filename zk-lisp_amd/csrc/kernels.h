@@ -57,6 +57,8 @@ void set_row_digest_rule(int rule);
 int row_digest_rule();
 // DIT passes on lazily reduced limbs (default) or the canonical kernel
 void set_ntt_lazy(bool on);
+const char* poseidon_build_config();  // poseidon.hip
+const char* kernels_build_config();   // kernels.hip
 // n Poseidon permutations of 12-element canonical states in place (engine as above)
 void launch_permute(fe* d_states, size_t n, int engine, hipStream_t s);
 struct CeParams;
@@ -81,9 +83,20 @@ void launch_hash_rows(const fe* d_mat, uint32_t n_cols, size_t n_rows, uint32_t 
 // Merkle tree: d_nodes[n..2n) must hold the leaves; fills d_nodes[1..n).
 void launch_merkle(fe* d_nodes, size_t n_leaves, hipStream_t s);
 // out[i] = merge_with_int(seed, base + 1 + i)   (RandomCoin::draw, counter base+1+i)
-void launch_draws(fe seed, uint64_t base, size_t k, fe* d_out, hipStream_t s);
+// d_seed != nullptr: the seed is read from device memory (the device-side transcript)
+void launch_draws(fe seed, uint64_t base, size_t k, fe* d_out, hipStream_t s, const fe* d_seed = nullptr);
 // smallest nonce in [base, base+count) with trailing_zeros(merge_with_int(seed, nonce)) >= bits
-void launch_grind(fe seed, uint64_t base, uint32_t count, uint32_t bits, unsigned long long* d_best, hipStream_t s);
+void launch_grind(fe seed, uint64_t base, uint32_t count, uint32_t bits, unsigned long long* d_best, hipStream_t s,
+                  const fe* d_seed = nullptr);
+// Device-side transcript (DefaultRandomCoin with the seed in device memory):
+// coin[0] = merge(coin[0], *value) and *value_out = *value (nullable)
+void launch_coin_reseed(fe* d_coin, const fe* d_value, fe* d_value_out, hipStream_t s);
+// FRI remainder coefficients (rem[0..rlen), highest degree first), their hash_elements
+// commitment rem[rlen], and coin[0] = merge(coin[0], rem[rlen]); wk[k] = w^-k, sk[k] = 3^-k / Nr
+void launch_fri_remainder(const fe* d_ev, uint32_t Nr, uint32_t rlen, const fe* wk, const fe* sk, fe* d_coin,
+                          fe* d_rem, hipStream_t s);
+// coin[1] = merge_with_int(coin[0], *d_best) when *d_best != ~0 (the query seed)
+void launch_query_seed(fe* d_coin, const unsigned long long* d_best, hipStream_t s);
 
 // ---- NTT ---------------------------------------------------------------------
 // Twiddle table in Montgomery/26-bit-limb form (entry = limbs of w * 2^156 mod p),

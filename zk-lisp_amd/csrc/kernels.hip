@@ -769,26 +769,33 @@ __global__ __launch_bounds__(256) void constraint_eval_pose_kernel(const fe* __r
 
 // out[i] = 1 / ((x_i - a1) (x_i - a2)^two) over the coset x_i = 3 w_M^i (w_M^i =
 // roots[i << shift]): each thread inverts INV_PTS points T apart with one field inversion
-// (Montgomery's trick), instead of one ~250-multiplication Fermat inversion per point.
+// (Montgomery's trick), instead of one ~250-multiplication Fermat inversion per point.  The
+// denominators are recomputed on the way back instead of kept: with both arrays live across the
+// inversion the compiler placed them in scratch (528 B per lane), and a kernel that needs scratch
+// makes the runtime allocate (and may reclaim) the queue's scratch between proofs.  The prefix
+// products go to the output slots instead (each slot k > 0 holds prefix k-1 until it is overwritten
+// with its inverse on the way back): 32 extra bytes per point of HBM traffic, no private array.
 constexpr int INV_PTS = 16;
+__device__ inline fe coset_den(const fe* __restrict__ roots, size_t i, int shift, fe a1, fe a2, int two) {
+  const fe x = fe_mul(fe{3, 0}, roots[i << shift]);
+  fe d = fe_sub(x, a1);
+  if (two) d = fe_mul(d, fe_sub(x, a2));
+  return d;
+}
 __global__ __launch_bounds__(256) void coset_inv_kernel(const fe* __restrict__ roots, int shift, fe a1, fe a2, int two,
                                                         fe* __restrict__ out) {
   const size_t T = (size_t)gridDim.x * blockDim.x;
   const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  fe den[INV_PTS], pre[INV_PTS];
-#pragma unroll
-  for (int k = 0; k < INV_PTS; k++) {
-    const fe x = fe_mul(fe{3, 0}, roots[(i0 + k * T) << shift]);
-    fe d = fe_sub(x, a1);
-    if (two) d = fe_mul(d, fe_sub(x, a2));
-    den[k] = d;
-    pre[k] = k ? fe_mul(pre[k - 1], d) : d;
+  fe pre = coset_den(roots, i0, shift, a1, a2, two);
+  for (int k = 1; k < INV_PTS; k++) {
+    out[i0 + k * T] = pre;  // prefix k-1
+    pre = fe_mul(pre, coset_den(roots, i0 + k * T, shift, a1, a2, two));
   }
-  fe inv = fe_inv(pre[INV_PTS - 1]);
-#pragma unroll
+  fe inv = fe_inv(pre);
   for (int k = INV_PTS - 1; k > 0; k--) {
-    out[i0 + k * T] = fe_mul(inv, pre[k - 1]);
-    inv = fe_mul(inv, den[k]);
+    const fe p = out[i0 + k * T];
+    out[i0 + k * T] = fe_mul(inv, p);
+    inv = fe_mul(inv, coset_den(roots, i0 + k * T, shift, a1, a2, two));
   }
   out[i0] = inv;
 }
@@ -1054,4 +1061,14 @@ void launch_gather(const uint64_t* d_addrs, size_t k, fe* d_out, hipStream_t s) 
   if (k) gather_kernel<<<(unsigned)((k + 255) / 256), 256, 0, s>>>(d_addrs, k, d_out);
 }
 
+}  // namespace zkl
+
+// compiled-in tuning values of this translation unit (zkl_hip_build_config)
+#define ZKL_STR2(x) #x
+#define ZKL_STR(x) ZKL_STR2(x)
+namespace zkl {
+const char* kernels_build_config() {
+  return "NTT_ELEMS=" ZKL_STR(NTT_ELEMS_CFG) ";NTT_THREADS=" ZKL_STR(NTT_THREADS_CFG) ";CE_WAVES=" ZKL_STR(
+      CE_WAVES_CFG) ";DEEP_PTS=" ZKL_STR(DEEP_PTS_CFG) ";DEEP_COLS=" ZKL_STR(DEEP_COLS_CFG);
+}
 }  // namespace zkl

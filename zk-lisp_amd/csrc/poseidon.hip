@@ -401,7 +401,8 @@ __global__ PG_KERNEL void merkle_level_kernel(fe* nodes, size_t lvl) {
   if (live && P.j == 0) nodes[i] = d;
 }
 
-__global__ PG_KERNEL void draw_kernel(fe seed, uint64_t base, size_t k, fe* out) {
+__global__ PG_KERNEL void draw_kernel(fe seed, const fe* seed_p, uint64_t base, size_t k, fe* out) {
+  if (seed_p) seed = *seed_p;
   PG_SETUP();
   const bool live = P.g < PG_PER_WAVE && item < k;
   const uint64_t ctr = base + 1 + item;
@@ -409,8 +410,9 @@ __global__ PG_KERNEL void draw_kernel(fe seed, uint64_t base, size_t k, fe* out)
   if (live && P.j == 0) out[item] = d;
 }
 
-__global__ PG_KERNEL void grind_kernel(fe seed, uint64_t base, uint32_t count, uint32_t bits,
+__global__ PG_KERNEL void grind_kernel(fe seed, const fe* seed_p, uint64_t base, uint32_t count, uint32_t bits,
                                                     unsigned long long* best) {
+  if (seed_p) seed = *seed_p;
   // an earlier window found one (every nonce of an earlier window is below base; a solution
   // this window's other blocks have already found is not a reason to stop)
   if (*(volatile unsigned long long*)best < base) return;
@@ -546,19 +548,98 @@ void launch_permute(fe* d_states, size_t n, int engine, hipStream_t s) {
     pg_permute_kernel<<<pg_blocks(n), 256, 0, s>>>(d_states, n);
 }
 
-void launch_draws(fe seed, uint64_t base, size_t k, fe* d_out, hipStream_t s) {
+void launch_draws(fe seed, uint64_t base, size_t k, fe* d_out, hipStream_t s, const fe* d_seed) {
   if (!k) return;
   if (hash_engine() == 1 && k >= pm_min_items())
-    PM_GO(draw_pm_kernel, k, false, s)(seed, base, k, d_out);
+    PM_GO(draw_pm_kernel, k, false, s)(seed, d_seed, base, k, d_out);
   else
-    draw_kernel<<<pg_blocks(k), 256, 0, s>>>(seed, base, k, d_out);
+    draw_kernel<<<pg_blocks(k), 256, 0, s>>>(seed, d_seed, base, k, d_out);
 }
 
-void launch_grind(fe seed, uint64_t base, uint32_t count, uint32_t bits, unsigned long long* d_best, hipStream_t s) {
+void launch_grind(fe seed, uint64_t base, uint32_t count, uint32_t bits, unsigned long long* d_best, hipStream_t s,
+                  const fe* d_seed) {
   if (hash_engine() == 1 && count >= pm_min_items())
-    PM_GO(grind_pm_kernel, count, false, s)(seed, base, count, bits, d_best);
+    PM_GO(grind_pm_kernel, count, false, s)(seed, d_seed, base, count, bits, d_best);
   else
-    grind_kernel<<<pg_blocks(count), 256, 0, s>>>(seed, base, count, bits, d_best);
+    grind_kernel<<<pg_blocks(count), 256, 0, s>>>(seed, d_seed, base, count, bits, d_best);
+}
+
+// ---- device transcript steps (DefaultRandomCoin on the device; one wave, group 0) --------
+// coin[0] = merge(coin[0], *v); *v_out = *v (the commitment, for the proof bytes)
+__global__ __launch_bounds__(64) void coin_reseed_kernel(fe* coin, const fe* v, fe* v_out) {
+  __shared__ __align__(16) uint32_t pw_lds[PW_WAVE_WORDS];
+  PWGroup P;
+  pw_init(P, pw_lds);
+  const bool live = P.g == 0;
+  const fe seed = coin[0], r = *v;
+  const fe s1 = pw_sponge<DOM_MERGE>(P, live, 2, [&](int j) { return j == 0 ? seed : r; });
+  if (threadIdx.x == 0) {
+    coin[0] = s1;
+    if (v_out) *v_out = r;
+  }
+}
+void launch_coin_reseed(fe* d_coin, const fe* d_value, fe* d_value_out, hipStream_t s) {
+  coin_reseed_kernel<<<1, 64, 0, s>>>(d_coin, d_value, d_value_out);
+}
+
+// FRI remainder (agg/trace.rs:926-952 geometry): the rlen lowest coefficients of the Nr last
+// evaluations over 3 <w_Nr> (c_k = sum_j ev_j w^-jk / Nr * 3^-k), stored highest degree first
+// in rem[0..rlen), rem[rlen] = hash_elements(rem), then coin[0] = merge(coin[0], rem[rlen]).
+struct RemArgs {
+  fe wk[16];   // w^-k, k < rlen
+  fe sk[16];   // 3^-k / Nr
+};
+__global__ __launch_bounds__(64) void fri_remainder_kernel(const fe* ev, uint32_t Nr, uint32_t rlen, RemArgs A, fe* coin,
+                                                           fe* rem) {
+  __shared__ __align__(16) uint32_t pw_lds[PW_WAVE_WORDS];
+  __shared__ fe c[16];
+  const uint32_t t = threadIdx.x;
+  if (t < rlen) {
+    fe acc = fe_zero(), p = fe_one();
+    for (uint32_t j = 0; j < Nr; j++) {
+      acc = fe_add(acc, fe_mul(ev[j], p));
+      p = fe_mul(p, A.wk[t]);
+    }
+    c[rlen - 1 - t] = fe_mul(acc, A.sk[t]);
+  }
+  __syncthreads();
+  PWGroup P;
+  pw_init(P, pw_lds);
+  const bool live = P.g == 0;
+  fe d = pw_sponge<DOM_ELEMS>(P, live, (int)((rlen + 1) / 2), [&](int j) {
+    return fold_pair(c[2 * j], (uint32_t)(2 * j + 1) < rlen ? c[2 * j + 1] : fe_zero());
+  });
+  d = pw_bcast(P, d, 0);
+  const fe seed = coin[0];
+  const fe s1 = pw_sponge<DOM_MERGE>(P, live, 2, [&](int j) { return j == 0 ? seed : d; });
+  if (t == 0) {
+    coin[0] = s1;
+    rem[rlen] = d;
+  }
+  if (t < rlen) rem[t] = c[t];
+}
+void launch_fri_remainder(const fe* d_ev, uint32_t Nr, uint32_t rlen, const fe* wk, const fe* sk, fe* d_coin, fe* d_rem,
+                          hipStream_t s) {
+  if (rlen < 1 || rlen > 16 || rlen > Nr) throw std::invalid_argument("FRI remainder: rem_deg + 1 must be in 1..16");
+  RemArgs A{};
+  for (uint32_t k = 0; k < rlen; k++) { A.wk[k] = wk[k]; A.sk[k] = sk[k]; }
+  fri_remainder_kernel<<<1, 64, 0, s>>>(d_ev, Nr, rlen, A, d_coin, d_rem);
+}
+
+// query seed: coin[1] = merge_with_int(coin[0], *best) when grinding found a nonce
+__global__ __launch_bounds__(64) void query_seed_kernel(fe* coin, const unsigned long long* best) {
+  __shared__ __align__(16) uint32_t pw_lds[PW_WAVE_WORDS];
+  const unsigned long long b = *best;
+  if (b == ~0ull) return;  // wave-uniform: no nonce yet, the host continues the search
+  PWGroup P;
+  pw_init(P, pw_lds);
+  const bool live = P.g == 0;
+  const fe seed = coin[0];
+  const fe q = pw_sponge<DOM_INT>(P, live, 2, [&](int j) { return j == 0 ? seed : fe{(uint64_t)b, 0}; });
+  if (threadIdx.x == 0) coin[1] = q;
+}
+void launch_query_seed(fe* d_coin, const unsigned long long* d_best, hipStream_t s) {
+  query_seed_kernel<<<1, 64, 0, s>>>(d_coin, d_best);
 }
 
 // FRI layer leaves: hash_elements([e_i, e_{i+Nd/2}]) (FriProver::build_layer, folding 2)
@@ -586,4 +667,19 @@ void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s) {
     fri_leaf_kernel<<<pg_blocks(h), 256, 0, s>>>(d_ev, h, d_leaves);
 }
 
+}  // namespace zkl
+
+// compiled-in tuning values of this translation unit (zkl_hip_build_config; every value is a
+// supported configuration, tests/test_abi.py checks the shipped build carries the defaults)
+#define ZKL_STR2(x) #x
+#define ZKL_STR(x) ZKL_STR2(x)
+#ifndef ZKL_POSEIDON_SCHED_NAME
+#define ZKL_POSEIDON_SCHED_NAME default
+#endif
+namespace zkl {
+const char* poseidon_build_config() {
+  return "PM_WAVES=" ZKL_STR(PM_WAVES_CFG) ";PM_WIDE=" ZKL_STR(PM_WIDE_CFG) ";PM_ROW_WAVES=" ZKL_STR(
+      PM_ROW_WAVES_CFG) ";PM_IGLP=" ZKL_STR(PM_IGLP_CFG) ";TAIL_PRIO=" ZKL_STR(TAIL_PRIO_CFG) ";PW_MAX_ITEMS=" ZKL_STR(
+      PW_MAX_ITEMS_CFG) ";PM_ROW_BIG=" ZKL_STR(PM_ROW_BIG_CFG) ";POSEIDON_SCHED=" ZKL_STR(ZKL_POSEIDON_SCHED_NAME);
+}
 }  // namespace zkl

@@ -80,6 +80,11 @@ struct HBuf {
 
 }  // namespace
 
+// pinned transcript staging (h_tx), in field elements: [0..4) seed + roots, [4..21) FRI
+// remainder + commitment, [32] seed upload, [40] best nonce, [48..80) FRI coins/roots,
+// [80..336) query draws, [336] FRI seed upload
+constexpr size_t TX_CS = 48, TX_CS_MAX = 32, TX_QD = 80, TX_QD_MAX = 256, TX_FRI_SEED = 336, TX_WORDS = 344;
+
 // ====================================================================== context
 struct zkl_ctx {
   int device = 0;
@@ -92,7 +97,7 @@ struct zkl_ctx {
   size_t tab_n = 0, tab_N = 0;
   DBuf roots, iroots, mroots, miroots, opow, opow_n, pertab;
   // work buffers
-  DBuf trace, coef, lde, parts, tree, ce, bvec, bm, clde, ctree, deep, draws, pw, oodv, oodf, asl, ast, asv, ars;
+  DBuf trace, coef, lde, parts, tree, ce, bvec, bm, clde, ctree, deep, draws, pw, oodv, oodf, txs, asl, ast, asv, ars;
   DBuf fri_ev, fri_tree, best, gaddr, gout, flag;
   DBuf xinv;    // batch-inverted coset denominators of DEEP (z-dependent)
   DBuf cexinv;  // 1 / (x - g^(n-1)) over the CE coset: shape-only, kept while the key matches
@@ -100,7 +105,7 @@ struct zkl_ctx {
   const void* cexinv_key_roots = nullptr;
   DBuf kconst;  // ProofConsts of the proof in flight on this context
   DBuf fri_coin;  // device transcript of the FRI layers: seed, alpha, layer roots
-  HBuf h_asrt, h_ood, h_addr, h_gv;  // pinned staging: assertions, OOD partial sums, gather plan/values
+  HBuf h_asrt, h_ood, h_addr, h_gv, h_tx, h_air;  // pinned staging: assertions, OOD frame, gather plan/values, transcript
   hipStream_t aux = nullptr;         // copy stream: assertion upload overlapped with the trace commitment
   hipEvent_t aux_ev = nullptr, hev = nullptr;
   // host-trace upload (zkl_hip_prove_segment): a ring of pinned slots, each filled from the
@@ -121,6 +126,10 @@ struct zkl_ctx {
   int ktiming = 1;  // 0: no kernel-family events, 1: trace row hash only, 2: every family
   double kfam_ms[ZKL_NUM_KFAMILIES] = {0};
   int kfam_n[ZKL_NUM_KFAMILIES] = {0};
+  // host scratch kept across proofs (gather plan, proof bytes): no per-proof allocation of the
+  // large host buffers
+  std::vector<uint64_t> addrs_s;
+  std::vector<uint8_t> proof_s;
 };
 
 static const char* kFamilyNames =
@@ -173,7 +182,9 @@ void set_err(zkl_ctx* c, const std::string& m) {
   g_global_err = g_tls_err.c_str();
 }
 
-// PoseidonHasher constants (suite [0;32]) in both device forms
+// PoseidonHasher constants (suite [0;32]) in both device forms: device globals, uploaded once
+// per device (every context of a device shares them; they never change), then synchronised, so
+// no proof carries a host-to-device copy of pageable memory (the runtime stages those)
 void upload_hasher(hipStream_t s) {
   static HasherConsts hc;
   static HasherMont hm;
@@ -186,8 +197,16 @@ void upload_hasher(hipStream_t s) {
     hc.dom_elems = H.dom_elems; hc.dom_merge = H.dom_merge; hc.dom_many = H.dom_many; hc.dom_int = H.dom_int;
     hm = make_hasher_mont(hc);
   });
+  static std::mutex mu;
+  static std::set<int> done;
+  int dev = 0;
+  HIPCHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  if (done.count(dev)) return;
   upload_hasher_mont(hm, s);
   upload_pm_tables(hc, s);
+  HIPCHECK(hipStreamSynchronize(s));
+  done.insert(dev);
 }
 
 void ensure_tables(zkl_ctx* C, size_t n, size_t N) {
@@ -476,6 +495,21 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   auto pie = pi_elements(pi);
   seed_el.insert(seed_el.end(), pie.begin(), pie.end());
   Coin coin{H.hash_elements(seed_el.data(), seed_el.size()), 0};
+  // The transcript up to the OOD point runs on the device: the seed goes up once, and the
+  // trace-root reseed and the composition-coefficient draws follow the trace tree with no host
+  // round trip (tx: [0] coin seed, [1] query seed, [2] trace root, [3] constraint root,
+  // [4..] FRI remainder + its commitment; h_tx mirrors it, h_tx[32] stages the upload).
+  // every per-proof copy goes through pinned memory (h_tx): an asynchronous copy to or from
+  // pageable memory makes the runtime stage it, which was seen to stall the stream
+  C->txs.ensure(64 * sizeof(fe));
+  C->h_tx.ensure(TX_WORDS * sizeof(fe));
+  fe* tx = C->txs.f();
+  fe* htx = C->h_tx.at<fe>();
+  htx[32] = coin.seed;
+  HIPCHECK(hipMemcpyAsync(tx, htx + 32, sizeof(fe), hipMemcpyHostToDevice, s));
+  launch_coin_reseed(tx, C->tree.f() + 1, tx + 2, s);
+  check_launch("trace-root reseed");
+  coin.counter = 0;  // coin.seed is on the device until the constraint root
   // The AIR instance (layout, degrees, ~2.9e5 assertions at n = 2^16) is built on the host
   // meanwhile too.
   AirInstance air;
@@ -492,7 +526,9 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   const int Cc = air.num_comp_cols;
   C->kconst.ensure(sizeof(ProofConsts));
   ProofConsts* dK = (ProofConsts*)C->kconst.p;
-  upload_air_consts(dK, air.dev, s);
+  C->h_air.ensure(sizeof(AirDevice));
+  memcpy(C->h_air.p, &air.dev, sizeof(AirDevice));
+  upload_air_consts(dK, *C->h_air.at<AirDevice>(), s);
   const size_t na = air.assertions.size();
   // boundary tables: per asserted column c, M_c = coset-LDE of
   // reverse(NTT_n(beta_c)); W likewise from sum_c beta*value.
@@ -533,10 +569,6 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->bvec.ensure((size_t)(nb + 1) * n * sizeof(fe));
   C->bm.ensure((size_t)(nb + 1) * ce * sizeof(fe));
   HT("air_built");
-  fe troot;
-  d2h(C, &troot, C->tree.f() + 1, sizeof(fe));
-  HT("troot");
-  coin.reseed(troot);
   T.mark(2);
 
   // ---- 2. composition coefficients (Linear): transition then boundary, one draw each
@@ -544,7 +576,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->draws.ensure((ndraw + 1024) * sizeof(fe));
   {
     KScope k(C, KF_MISC);
-    launch_draws(coin.seed, coin.counter, ndraw, C->draws.f(), s);
+    launch_draws(fe_zero(), coin.counter, ndraw, C->draws.f(), s, tx);
   }
   check_launch("composition coefficient draws");
   coin.counter += ndraw;
@@ -633,17 +665,22 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     KScope k(C, KF_MERKLE);
     launch_merkle(C->ctree.f(), N, s);
   }
+  launch_coin_reseed(tx, C->ctree.f() + 1, tx + 3, s);
   check_launch("composition commitment");
+  // one round trip: degree flag, both roots and the coin seed after the constraint root
+  HIPCHECK(hipMemcpyAsync(htx, tx, 4 * sizeof(fe), hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipMemcpyAsync(htx + 4, C->flag.p, 4, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  HT("croot");
   unsigned bad = 0;
-  d2h(C, &bad, C->flag.p, 4);
+  memcpy(&bad, htx + 4, 4);
   if (bad) throw InvalidArg("constraint composition polynomial degree too large: trace does not satisfy the AIR");
-  fe croot;
-  d2h(C, &croot, C->ctree.f() + 1, sizeof(fe));
-  coin.reseed(croot);
+  const fe troot = htx[2], croot = htx[3];
+  coin.seed = htx[0];
+  coin.counter = 0;
   T.mark(4);
 
   // ---- 4. OOD frame at z and z*g
-  HT("croot");
   fe z = coin.draw(), zg = fe_mul(z, g);
   C->pw.ensure(4 * n * sizeof(fe));
   fe* pw = C->pw.f();
@@ -735,7 +772,8 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   std::vector<fe> fri_roots(nl);
   C->fri_coin.ensure((2 + (size_t)nl) * sizeof(fe));
   fe* d_coin = C->fri_coin.f();
-  HIPCHECK(hipMemcpyAsync(d_coin, &coin.seed, sizeof(fe), hipMemcpyHostToDevice, s));
+  htx[TX_FRI_SEED] = coin.seed;
+  HIPCHECK(hipMemcpyAsync(d_coin, htx + TX_FRI_SEED, sizeof(fe), hipMemcpyHostToDevice, s));
   for (int d = 0; d < nl; d++) {
     size_t Nd = N >> d, h = Nd / 2;
     fe* tr = C->fri_tree.f() + tr_off[d];
@@ -753,75 +791,87 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   }
   check_launch("FRI layers");
   HT("fri_enqueued");
-  size_t Nr = N >> nl;
-  std::vector<fe> rem_ev(Nr), cs(2 + (size_t)nl);
-  // the layer coins / roots and the remainder evaluations in one round trip
-  if (nl > 0) HIPCHECK(hipMemcpyAsync(cs.data(), d_coin, cs.size() * sizeof(fe), hipMemcpyDeviceToHost, s));
-  d2h(C, rem_ev.data(), layer_ev(nl), Nr * sizeof(fe));
-  if (nl > 0) {
-    for (int d = 0; d < nl; d++) fri_roots[d] = cs[2 + d];
-    coin.seed = cs[0];
-    coin.counter = 1;
-  }
-  // interpolate over 3*<w_Nr> (constant domain offset, agg/trace.rs:940-952), keep rem_deg+1, reversed
-  std::vector<fe> rc(Nr);
+  // FRI remainder, its commitment and the reseed, grinding, the query seed and the query draws
+  // all follow the layer chain on the device; the host reads the results back once
+  const size_t Nr = N >> nl;
+  const uint32_t rlen = o.fri_remainder_max_degree + 1;
   {
-    fe w = root_of_unity(ilog2(Nr)), wi = fe_inv(w), inv_nr = fe_inv(fe{Nr, 0});
-    for (size_t k = 0; k < Nr; k++) {
-      fe acc = fe_zero(), wk = fe_pow64(wi, k), p = fe_one();
-      for (size_t j = 0; j < Nr; j++) { acc = fe_add(acc, fe_mul(rem_ev[j], p)); p = fe_mul(p, wk); }
-      rc[k] = fe_mul(fe_mul(acc, inv_nr), fe_pow64(inv3, k));
+    const fe w = root_of_unity(ilog2(Nr)), wi = fe_inv(w), inv_nr = fe_inv(fe{Nr, 0});
+    fe wk[16], sk[16];
+    for (uint32_t k = 0; k < rlen; k++) {
+      wk[k] = fe_pow64(wi, k);
+      sk[k] = fe_mul(inv_nr, fe_pow64(inv3, k));
     }
+    KScope k(C, KF_FRI);
+    launch_fri_remainder(layer_ev(nl), (uint32_t)Nr, rlen, wk, sk, d_coin, tx + 4, s);
   }
-  const size_t rlen = o.fri_remainder_max_degree + 1;
-  std::vector<fe> rem(rlen);
-  for (size_t k = 0; k < rlen; k++) rem[k] = rc[rlen - 1 - k];
-  HT("rem");
-  fe rem_commit = H.hash_elements(rem.data(), rlen);
-  coin.reseed(rem_commit);
+  check_launch("FRI remainder");
   T.mark(7);
 
   // ---- 7. grinding: smallest nonce >= 1 (winterfell without `concurrent`)
   HT("grind_start");
   uint64_t nonce = 0;
   C->best.ensure(8);
-  if (o.grinding_factor == 0) {
-    nonce = 1;
-  } else {
-    // Ascending windows of nonces; the answer is the minimum of the first window that holds a
-    // solution.  Four windows (2^g, 2^g, 2^(g+1), 2^(g+2) tries) are queued per read-back, and
-    // a window's kernel returns at once when an earlier one has already found a solution
-    // (grind kernels check *best first), so the search costs the windows it needs plus a few
-    // empty launches, and one read-back settles it with probability 1 - e^-8.  A window of
-    // 2^16 tries is one permutation's latency on the chip (~0.45 ms); the expected cost is
-    // (1 + e^-1 + 2 e^-2 + 4 e^-4) windows = 1.7 instead of the 2.6 of one 2^(g+1) window first
-    // and doubling windows after it.
-    uint32_t batch = 1u << std::min<uint32_t>(std::max<uint32_t>(o.grinding_factor, 14), 22);
-    for (uint64_t base = 1; nonce == 0;) {
-      unsigned long long init = ~0ull;
-      HIPCHECK(hipMemcpyAsync(C->best.p, &init, 8, hipMemcpyHostToDevice, s));
-      KScope k(C, KF_GRIND);
-      for (int w = 0; w < 4; w++) {
-        launch_grind(coin.seed, base, batch, o.grinding_factor, (unsigned long long*)C->best.p, s);
-        base += batch;
-        if (w >= 1) batch = std::min<uint32_t>(batch * 2, 1u << 22);
-      }
-      check_launch("grinding");
-      unsigned long long r = 0;
-      d2h(C, &r, C->best.p, 8);
-      if (r != ~0ull) nonce = r;
+  unsigned long long* hbest = (unsigned long long*)(htx + 40);
+  // Ascending windows of nonces; the answer is the minimum of the first window that holds a
+  // solution.  Four windows (2^g, 2^g, 2^(g+1), 2^(g+2) tries) are queued per read-back, and a
+  // window's kernel returns at once when an earlier one has already found a solution (grind
+  // kernels check *best first), so the search costs the windows it needs plus a few empty
+  // launches, and one read-back settles it with probability 1 - e^-8.  A window of 2^16 tries is
+  // one permutation's latency on the chip (~0.45 ms); the expected cost is (1 + e^-1 + 2 e^-2 +
+  // 4 e^-4) windows = 1.7 instead of the 2.6 of one 2^(g+1) window first and doubling after it.
+  // grinding factor 0: the first candidate, nonce 1.
+  uint32_t batch = 1u << std::min<uint32_t>(std::max<uint32_t>(o.grinding_factor, 14), 22);
+  uint64_t base = 1;
+  auto queue_windows = [&](const fe* d_seed, fe h_seed) {
+    *hbest = o.grinding_factor == 0 ? 1ull : ~0ull;
+    HIPCHECK(hipMemcpyAsync(C->best.p, hbest, 8, hipMemcpyHostToDevice, s));
+    if (o.grinding_factor == 0) return;
+    KScope k(C, KF_GRIND);
+    for (int w = 0; w < 4; w++) {
+      launch_grind(h_seed, base, batch, o.grinding_factor, (unsigned long long*)C->best.p, s, d_seed);
+      base += batch;
+      if (w >= 1) batch = std::min<uint32_t>(batch * 2, 1u << 22);
     }
+  };
+  queue_windows(d_coin, fe_zero());
+  launch_query_seed(d_coin, (const unsigned long long*)C->best.p, s);
+  launch_draws(fe_zero(), 0, o.num_queries, C->draws.f(), s, d_coin + 1);
+  check_launch("grinding and query draws");
+  // one read-back: layer coins / roots, remainder + commitment, nonce, query draws
+  if (2 + (size_t)nl > TX_CS_MAX || o.num_queries > TX_QD_MAX) throw std::runtime_error("internal: transcript staging");
+  HIPCHECK(hipMemcpyAsync(htx + TX_CS, d_coin, (2 + (size_t)nl) * sizeof(fe), hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipMemcpyAsync(htx + 4, tx + 4, (rlen + 1) * sizeof(fe), hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipMemcpyAsync(hbest, C->best.p, 8, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipMemcpyAsync(htx + TX_QD, C->draws.p, o.num_queries * sizeof(fe), hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  std::vector<fe> cs(htx + TX_CS, htx + TX_CS + 2 + nl), qd(htx + TX_QD, htx + TX_QD + o.num_queries);
+  for (int d = 0; d < nl; d++) fri_roots[d] = cs[2 + d];
+  std::vector<fe> rem(htx + 4, htx + 4 + rlen);
+  const fe rem_commit = htx[4 + rlen];
+  coin.seed = cs[0];  // after the remainder reseed
+  coin.counter = 0;
+  HT("rem");
+  if (*hbest != ~0ull) {
+    nonce = *hbest;
+  } else {  // none in the first four windows (probability e^-8): continue from the host
+    while (nonce == 0) {
+      queue_windows(nullptr, coin.seed);
+      check_launch("grinding");
+      HIPCHECK(hipMemcpyAsync(hbest, C->best.p, 8, hipMemcpyDeviceToHost, s));
+      HIPCHECK(hipStreamSynchronize(s));
+      if (*hbest != ~0ull) nonce = *hbest;
+    }
+    launch_draws(H.merge_with_int(coin.seed, nonce), 0, o.num_queries, C->draws.f(), s);
+    check_launch("query draws");
+    HIPCHECK(hipMemcpyAsync(htx + TX_QD, C->draws.p, o.num_queries * sizeof(fe), hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    qd.assign(htx + TX_QD, htx + TX_QD + o.num_queries);
   }
   T.mark(8);
 
   // ---- 8. query positions: draw_integers(q, N, nonce), sort, dedup
   HT("q_start");
-  coin.seed = H.merge_with_int(coin.seed, nonce);
-  coin.counter = 0;
-  std::vector<fe> qd(o.num_queries);
-  launch_draws(coin.seed, 0, o.num_queries, C->draws.f(), s);
-  check_launch("query draws");
-  d2h(C, qd.data(), C->draws.p, qd.size() * sizeof(fe));
   HT("q_drawn");
   std::vector<size_t> pos;
   for (auto& v : qd) pos.push_back((size_t)(v.lo & (N - 1)));
@@ -831,7 +881,8 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
 
   HT("q_sorted");
   // gather plan: trace rows, comp rows, trace/comp tree nodes, FRI values + tree nodes
-  std::vector<uint64_t> addrs;
+  std::vector<uint64_t>& addrs = C->addrs_s;
+  addrs.clear();
   addrs.reserve(nq * ((size_t)W + Cc) + 2 * nq * (size_t)(logN + 2) * (nl + 2) + 64);
   auto A = [&](const fe* p) { addrs.push_back((uint64_t)(uintptr_t)p); };
   for (size_t k = 0; k < nq; k++)
@@ -875,6 +926,8 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
 
   // ---- 9. Proof::to_bytes  [WF-recall layout, DESIGN.md §Proof bytes]
   Bytes P;
+  P.v.swap(C->proof_s);
+  P.v.clear();
   P.v.reserve(na_g * 32 + 4096);
   P.u8((uint8_t)W); P.u8(0); P.u8(0); P.u8((uint8_t)logn); P.u8(0); P.u8(0);  // TraceInfo
   P.u8(16); P.felem(fe{P_LO, P_HI});                                           // modulus bytes
@@ -937,7 +990,8 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   T.finish();
   HT("stage_events");
   resolve_kernel_times(C);
-  out.swap(P.v);
+  out.assign(P.v.begin(), P.v.end());
+  C->proof_s.swap(P.v);
   HT("returned");
   C->host_ms[2] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call0).count();
   {
@@ -980,6 +1034,11 @@ extern "C" {
 
 int zkl_hip_abi_version(void) { return ZKL_ABI_VERSION; }
 
+const char* zkl_hip_build_config(void) {
+  static const std::string cfg = std::string(poseidon_build_config()) + ";" + kernels_build_config();
+  return cfg.c_str();
+}
+
 int zkl_hip_init(int device, zkl_ctx** out) {
   if (!out) return ZKL_E_INVALID;
   *out = nullptr;
@@ -988,6 +1047,18 @@ int zkl_hip_init(int device, zkl_ctx** out) {
     HIPCHECK(hipGetDeviceCount(&cnt));
     if (device < 0 || device >= cnt) throw InvalidArg("no such HIP device");
     HIPCHECK(hipSetDevice(device));
+    // The transcript's host round trips wait on short device tails; a blocking (interrupt)
+    // wait there was seen to wake 20-30 ms late on some boxes.  Spin-waiting costs one host core
+    // per waiting context.  ZKL_SPIN=0 keeps the runtime's default; the flag only takes effect
+    // before the device's primary context exists, later calls fail harmlessly.
+    {
+      static std::once_flag once;
+      std::call_once(once, [] {
+        const char* e = getenv("ZKL_SPIN");
+        if (!(e && !strcmp(e, "0"))) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+        (void)hipGetLastError();
+      });
+    }
     auto* c = new zkl_ctx();
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
