@@ -26,10 +26,15 @@ Moves, selects and address arithmetic are free in every option (as in the floor)
      36 v_fma_f64 per product; the REDC steps also in f64 (floor / fma splitting per digit).
   E  24-bit integer products: 6 x 24-bit limbs, each 48-bit product as v_mad_u32_u24 (low 32)
      + v_mul_hi_u32_u24 (high 16) accumulated in 32-bit column pairs.
-  F  4 x 32-bit words (p = 1 mod 2^32: REDC digit m = -t0 mod 2^32 with no multiply, values kept
-     below 2^128 so the cube packs into 16 bytes with no top byte): 16 / 10 v_mad_u64_u32 per
-     product, but the 64-bit products overflow 64-bit columns, so each enters a 96-bit column
-     accumulator through a carry-out and an addc, and the columns are carried afterwards.
+  F  4 x 32-bit words (p = 1 mod 2^32: REDC digit m = -t0 mod 2^32 with no multiply; cube packed
+     into 16 bytes with no top byte after a conditional correction, so 6 k-steps per tile).  A
+     32 x 32 product is 64 bits, so columns cannot stay lazy as with 26-bit limbs: every product
+     enters its column through a 64-bit add (schoolbook rows: v_mad_u64_u32 + the running carry),
+     and the REDC keeps signed 64-bit columns (per digit: negate, 64-bit add, 64-bit shift, 64-bit
+     add, one v_mad_i64_i32 for m * 11520, 64-bit add of m at word i+4), then carries four words
+     and folds the top bit.  Round 4 first priced these carries as 32-bit add-with-carry ops
+     (1.109x, "build it"); counted with the 64-bit operations they need (v_lshl_add_u64 class,
+     half the v_add_u32 rate, about the v_mad_u64_u32 rate) the option is slower than A.
 
     python tools/arith_cost.py > profiles/r04/arith_cost.json
 """
@@ -96,21 +101,17 @@ def options():
     E = {"ops": add({"u24lo": 21, "u24hi": 21}, {"u24lo": 36, "u24hi": 36}, {"alu32": 2 * 24},
                     {"u24lo": 2 * 12, "u24hi": 2 * 12, "alu32": 2 * 20}, fold, pack16),
          "mfma_per_wave_round": 42}
-    # F (product scanning, the form whose carries parallelise across columns): each 64-bit
-    # product enters its column's 96-bit accumulator by v_mad_u64_u32 with carry-out + one addc
-    # (2 ops); the 8 columns are then carried (3 ops each).  Square: 4 squares + 6 cross products,
-    # cross columns doubled (3 ops per column, 7 columns).  REDC (R = 2^128, almost-Montgomery:
-    # inputs < 2^128, output < 2^128 + p, one conditional + c0 = 45*2^40 - 1 correction, 6 ops):
-    # 4 digits of m = -t0 (free), carry flag, m * 11520 at word 1 (1 mad), carries into words
-    # 3..5 and + m at word 4 (~5 ops).  Fold: 4 words of two digit pairs (2 ops + 1 mad), 4
-    # carries (3 ops), top * c0 (1 mad + 4), the correction (6).  Pack: 4 xors, no top byte, so
-    # the MDS needs 6 k-steps per tile instead of 7.
-    F = {"ops": add({"mad": 16, "alu32": 16 + 24}, {"mad": 10, "alu32": 10 + 21 + 24},
-                    {"mad": 2 * 4, "alu32": 2 * (4 * 5 + 6)}, {"mad": 6, "alu32": 4 * 2 + 4 * 3 + 4 + 6},
-                    {"alu32": 4}),
+    # F: square 10 products (mad + 64-bit accumulate each), cross terms doubled (7 64-bit
+    # shifts), diagonal carried in (8 alu32); REDC: 4 x (1 alu32 + 4 alu64 + 1 mad) + 4 word
+    # carries (8 alu64) + top fold (6 alu32); multiply 16 products (mad + 64-bit accumulate);
+    # second REDC as the first; fold of the digit columns into 4 words: 8 mads (digit pairs), 4
+    # carries (8 alu64), top fold 8 alu32; pack 4 xors
+    redc32 = {"mad": 4, "alu64": 16 + 8, "alu32": 4 + 6}
+    F = {"ops": add({"mad": 10, "alu64": 10 + 7, "alu32": 8}, redc32, {"mad": 16, "alu64": 16}, redc32,
+                    {"mad": 8, "alu64": 8, "alu32": 8}, {"alu32": 4}),
          "mfma_per_wave_round": 36}
     return {"A_current_26bit_montgomery": A, "B_toeplitz_mfma_square": B, "C_unreduced_cube_into_mds_mfma": C,
-            "D_f64_fma_limbs": D, "E_u24_products": E, "F_32bit_limbs_carry_chains": F}
+            "D_f64_fma_limbs": D, "E_u24_products": E, "F_32bit_words": F}
 
 
 def main():
@@ -136,10 +137,13 @@ def main():
                                 "relative_to_current": round(base / bound, 3)}
     best = max(out["options"].items(), key=lambda kv: kv[1]["relative_to_current"])
     gain = best[1]["relative_to_current"]
+    fewer = [k for k, v in out["options"].items() if v["valu_instr_per_element_round"] < 168 and not k.startswith("A_")]
+    out["valu_count_below_floor"] = fewer
     out["verdict"] = (f"best: {best[0]} at {gain}x the current arithmetic; "
                       + ("none of the alternatives beats the current one: not built" if best[0].startswith("A_") else
-                         "within the model's error (< 5%) and its 96-bit column carries are serial chains through "
-                         "carry SGPRs, which the two-waves-per-SIMD kernel cannot hide: not built" if gain < 1.05
+                         "within the model's error (< 5%), and it needs more MFMAs per round and nearly twice the LDS "
+                         "operand traffic (13 A fragments per tile instead of 7) with ~24 more live VGPRs in a kernel "
+                         "already at ~206: not built" if gain < 1.05
                          else "build it"))
     print(json.dumps(out, indent=1))
 
