@@ -258,7 +258,7 @@ def valu_roofline(perms_per_s):
 
 def load_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed PMC summary of the newest round."""
-    for r in ("r03", "r02", "r01"):
+    for r in ("r04", "r03", "r02", "r01"):
         p = os.path.join(ROOT, "profiles", r, "pmc_traffic.json")
         try:
             d = json.load(open(p))
@@ -388,6 +388,9 @@ def real_program(zkl_hip, device, steps, name="rollup-bench", max_rows=1 << 16):
             proof = ctx.prove_segment_device(d, sw, m, spi, o)
         ctx.synchronize()
         dt = time.perf_counter() - t0
+        ctx.set_kernel_timing(2)  # per-family breakdown from one extra, untimed proof
+        ctx.prove_segment_device(d, sw, m, spi, o)
+        fam = {k: round(v[0], 3) for k, v in ctx.kernel_times().items()}
     finally:
         ctx.free(d)
         ctx.close()
@@ -399,7 +402,8 @@ def real_program(zkl_hip, device, steps, name="rollup-bench", max_rows=1 << 16):
                       f"partitions ({o.num_partitions},{o.hash_rate}); op list from the compiler restatement",
             "value": round(steps / dt, 4), "unit": "segment-proofs/s", "ms_per_proof": round(dt / steps * 1e3, 3),
             "steps": steps, "rows": m, "width": sw, "proof_bytes": len(proof),
-            "parity": "match" if got == want else "MISMATCH", "golden": "tests/golden/programs.json (CPU oracle)"}
+            "parity": "match" if got == want else "MISMATCH", "golden": "tests/golden/programs.json (CPU oracle)",
+            "kernel_ms_per_family_untimed_step": fam}
 
 
 class Pipeline:
@@ -615,10 +619,12 @@ def main():
     dist.barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
-    step_ms = []
+    step_ms, step_stages = [], []
     for i in range(args.steps):
         proof = ctx.prove_segment_device(d_trace, W, n, pi, opts)
         step_ms.append(ctx.host_times()["call"])
+        if os.environ.get("ZKL_BENCH_STAGES"):
+            step_stages.append({k: round(v, 2) for k, v in ctx.stage_times().items()})
         for k, (ms, cnt) in ctx.kernel_times().items():
             a = kacc.setdefault(k, [0.0, 0])
             a[0] += ms
@@ -770,6 +776,7 @@ def main():
             "stage_ms_untimed_step": {k: round(v, 3) for k, v in stages.items()},
             "host_ms_last_step": {k: round(v, 3) for k, v in host.items()},
             "call_ms_each_step": [round(v, 2) for v in step_ms],
+            **({"stage_ms_each_step": step_stages} if step_stages else {}),
             "step_handoff": hand,
         }
         if c4 is not None:

@@ -18,9 +18,15 @@ struct AirAcc {
   __host__ __device__ __forceinline__ void emit(fe v) { mul_acc(al[ix++], v, a); }
 };
 
-template <bool POSE, bool RM, class Cur, class Nxt>
+// pose_k: K_j = sum_i alpha_{12j+i} rc[j][i] for the 27 Poseidon rounds (pose_k_kernel, once per
+// proof), or nullptr to form them here (host verifier).
+// PART: 0 = the whole sum; 1 = the PoseidonAir block alone; 2 = everything after it (its alphas
+// skipped).  Parts 1 + 2 = part 0: the device evaluates the Poseidon block in a kernel of its own,
+// whose register footprint does not add to the rest's.
+constexpr int pose_block_constraints(const AirDevice& a) { return 27 * 12 + 12 + (a.pose_bind ? 10 : 0); }
+template <bool POSE, bool RM, int PART = 0, class Cur, class Nxt>
 __host__ __device__ __forceinline__ fe air_transition_sum(const AirDevice& c_air, Cur cur, Nxt nxt, const fe* per,
-                                                          fe p_last, const fe* alpha) {
+                                                          fe p_last, const fe* alpha, const fe* pose_k = nullptr) {
   const Layout& C = c_air.cols;
   fe p_map = per[0], p_final = per[28], p_pad = per[29], p_pad_last = per[30];
   fe s_low = fe_mul(p_last, p_map);
@@ -36,7 +42,8 @@ __host__ __device__ __forceinline__ fe air_transition_sum(const AirDevice& c_air
   A.al = alpha;
   const fe one = fe_one();
 
-  if (POSE) {
+  if (POSE && PART == 2) A.ix += pose_block_constraints(c_air);
+  if (POSE && PART != 2) {
     // ---------------- PoseidonAir (poseidon.rs:65-162): y = MDS s^3 (+ rc_j) is the same
     // for all 27 rounds but the round constant, so it is formed once per point
     const fe pa = cur(C.pose_active);
@@ -50,11 +57,28 @@ __host__ __device__ __forceinline__ fe air_transition_sum(const AirDevice& c_air
       for (int k = 0; k < 12; k++) mul_acc(c_air.pose_mds[i][k], s3[k], acc);
       ms[i] = reduce288(acc);
     }
+    // constraint (j, i) = g_j (nxt_i - ms_i - rc_ji), g_j = pa per_j; its alpha-weighted sum over
+    // i is g_j (sum_i alpha_ji d_i - K_j) with d_i = nxt_i - ms_i: one lazy dot product and one
+    // product per round instead of 12 reduced products (the sum is the same field element)
+    fe d[12];
+#pragma unroll
+    for (int i = 0; i < 12; i++) d[i] = fe_sub(nxt(C.lanes_start + i), ms[i]);
+    const fe* al = A.al + A.ix;
     for (int j = 0; j < 27; j++) {
-      const fe g = fe_mul(pa, per[1 + j]);
-      for (int i = 0; i < 12; i++)
-        A.emit(fe_mul(g, fe_sub(nxt(C.lanes_start + i), fe_add(ms[i], c_air.pose_rc[j][i]))));
+      uint32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int i = 0; i < 12; i++) mul_acc(al[12 * j + i], d[i], acc);
+      fe kj;
+      if (pose_k) {
+        kj = pose_k[j];
+      } else {
+        uint32_t ka[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < 12; i++) mul_acc(al[12 * j + i], c_air.pose_rc[j][i], ka);
+        kj = reduce288(ka);
+      }
+      mul_acc(fe_mul(pa, per[1 + j]), fe_sub(reduce288(acc), kj), A.a);
     }
+    A.ix += 27 * 12;
     const fe g_hold = fe_sub_sel(p_pad, p_pad_last);
     for (int i = 0; i < 12; i++) A.emit(fe_mul(g_hold, fe_sub(nxt(C.lanes_start + i), cur(C.lanes_start + i))));
     if (c_air.pose_bind) {
@@ -77,6 +101,7 @@ __host__ __device__ __forceinline__ fe air_transition_sum(const AirDevice& c_air
       }
     }
   }
+  if (PART == 1) return reduce288(A.a);
 
   if (c_air.feat_vm) {
     // ---------------- VmCtrlAir (ctrl.rs:114-390)
@@ -84,15 +109,15 @@ __host__ __device__ __forceinline__ fe air_transition_sum(const AirDevice& c_air
     fe s_high = fe_mul(s_low, pi);
     fe sum_d0 = fe_zero(), sum_a = fe_zero(), sum_b = fe_zero(), sum_c = fe_zero(), sum_d1 = fe_zero();
     for (int r = 0; r < 8; r++) {
-      fe v[5] = {cur(C.sel_dst0 + r), cur(C.sel_a + r), cur(C.sel_b + r), cur(C.sel_c + r), cur(C.sel_dst1 + r)};
-      sum_d0 = fe_add_sel(sum_d0, v[0]); sum_a = fe_add_sel(sum_a, v[1]); sum_b = fe_add_sel(sum_b, v[2]);
-      sum_c = fe_add_sel(sum_c, v[3]); sum_d1 = fe_add_sel(sum_d1, v[4]);
-#pragma unroll
-      for (int t = 0; t < 5; t++) A.emit(fe_add_sel(fe_mul(p_map, fe_mul(v[t], fe_sub_sel(v[t], one))), s_high));
+      const fe v0 = cur(C.sel_dst0 + r), v1 = cur(C.sel_a + r), v2 = cur(C.sel_b + r), v3 = cur(C.sel_c + r),
+               v4 = cur(C.sel_dst1 + r);
+      sum_d0 = fe_add_sel(sum_d0, v0); sum_a = fe_add_sel(sum_a, v1); sum_b = fe_add_sel(sum_b, v2);
+      sum_c = fe_add_sel(sum_c, v3); sum_d1 = fe_add_sel(sum_d1, v4);
+      auto bit = [&](fe v) { A.emit(fe_add_sel(fe_mul(p_map, fe_mul(v, fe_sub_sel(v, one))), s_high)); };
+      bit(v0); bit(v1); bit(v2); bit(v3); bit(v4);
     }
     // op bits read through cur() wherever used: a local fe[17] indexed in the loops below was
-    // placed in scratch (288 B per lane), and a kernel that needs scratch makes the runtime
-    // allocate the queue's scratch memory on a later dispatch
+    // placed in scratch (288 B per lane)
     auto bo = [&](int k) { return cur(C.op[k]); };
     enum { CONST, MOV, ADD, SUB, MUL, NEG, EQ, SEL, SPONGE, ASSERT, ABIT, ARANGE, DIVMOD, DIV128, MULWIDE, LOAD, STORE };
     fe uses_a = fe_add_sel(fe_add_sel(fe_add_sel(bo(MOV), bo(ADD)), fe_add_sel(bo(SUB), bo(MUL))), fe_add_sel(fe_add_sel(bo(NEG), bo(EQ)), bo(SEL)));

@@ -62,15 +62,18 @@ const char* kernels_build_config();   // kernels.hip
 // n Poseidon permutations of 12-element canonical states in place (engine as above)
 void launch_permute(fe* d_states, size_t n, int engine, hipStream_t s);
 struct CeParams;
+struct DerivedConsts;
 struct ProofConsts;  // per-proof constants in device memory, one block per context (below)
 void upload_air_consts(ProofConsts* dK, const AirDevice& a, hipStream_t s);
 // transition composition coefficients alpha_j: copied device->device from the draw buffer
 void upload_alphas_from_device(ProofConsts* dK, const fe* d_alphas, int n, hipStream_t s);
-void upload_deep_coeffs(ProofConsts* dK, const fe* h_coeffs, int n, hipStream_t s);
-// The DEEP coefficients straight from the draw buffer (no host round trip): dK->deep,
-// dK->deep_m (limbs of g * 2^156) and dK->deep_sz from the OOD frame d_frame (t(z) [W] | H(z) [C]
+// dK->pose_k from dK->alpha and the AIR's round constants (after upload_alphas_from_device; the
+// Poseidon block's alphas come first in the evaluation order)
+void launch_pose_k(const ProofConsts* dK, DerivedConsts* dD, hipStream_t s);
+// The DEEP coefficients straight from the draw buffer (no host round trip): dD->deep,
+// dD->deep_m (limbs of g * 2^156) and dD->deep_sz from the OOD frame d_frame (t(z) [W] | H(z) [C]
 // | t(zg) [W] | H(zg) [C]).  n = W + C <= 256.
-void launch_deep_coeffs(const fe* d_gam, uint32_t W, uint32_t C, const fe* d_frame, ProofConsts* dK, hipStream_t s);
+void launch_deep_coeffs(const fe* d_gam, uint32_t W, uint32_t C, const fe* d_frame, DerivedConsts* dD, hipStream_t s);
 
 // ---- hashing --------------------------------------------------------------
 // Row digests of a column-major matrix (ld = rows per column) with Winterfell partitioning.
@@ -172,15 +175,20 @@ struct ProofConsts {
   AirDevice air;
   CeParams ce;
   fe alpha[1024];  // transition composition coefficients
-  fe deep[512];   // DEEP coefficients (trace then composition columns)
+};
+// Per-proof constants the device derives itself (written by kernels, read by later kernels),
+// kept apart from ProofConsts, which only host/device copies write.
+struct DerivedConsts {
+  fe pose_k[27];            // sum_i alpha_{12j+i} rc[j][i] per Poseidon round (launch_pose_k)
+  fe deep[512];             // DEEP coefficients (trace then composition columns)
   uint32_t deep_m[512][5];  // the same as 26-bit limbs of g * 2^156 mod p (deep_kernel)
-  fe deep_sz[2];  // sum_i g_i * frame_i(z), sum_i g_i * frame_i(z g) (deep_coeffs_kernel)
+  fe deep_sz[2];            // sum_i g_i * frame_i(z), sum_i g_i * frame_i(z g) (deep_coeffs_kernel)
 };
 void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab,
                             const fe* d_bm /* (n_bcols + 1) x ce */, const CeParams& p, ProofConsts* dK,
-                            bool pose_block, bool ram_merkle,
+                            const DerivedConsts* dD, bool pose_block, bool ram_merkle,
                             fe* d_xinv /* ce entries: 1 / (x_i - g^(n-1)) */, bool xinv_ready, fe* d_out,
-                            hipStream_t s, int split = 0);
+                            hipStream_t s, int split = 0, fe* d_pose_part /* ce entries, Poseidon layouts */ = nullptr);
 // boundary vectors: vec[slot*n + step] = beta_a ; wv[s] = sum beta_a*value_a over assertions at step s
 void launch_boundary_scatter(const uint32_t* d_slot, const uint32_t* d_step, const fe* d_beta, size_t n_assert,
                              size_t n, fe* d_vecs, hipStream_t s);
@@ -205,7 +213,7 @@ void launch_ood(const OodArgs& a, fe* d_partial, hipStream_t s);
 // mult[j]; written in transcript order t(z) [W] | H(z) [C] | t(zg) [W] | H(zg) [C].
 void launch_ood_frame(const fe* d_partial_trace, const fe* d_partial_comp, uint32_t W, uint32_t C, uint32_t chunks,
                       const fe* mult /* C host values */, fe* d_frame, hipStream_t s);
-struct DeepParams {  // the frame dot products come from ProofConsts::deep_sz (launch_deep_coeffs)
+struct DeepParams {  // the frame dot products come from DerivedConsts::deep_sz (launch_deep_coeffs)
   size_t N;
   uint32_t W, C;
   fe z, zg;
@@ -213,7 +221,7 @@ struct DeepParams {  // the frame dot products come from ProofConsts::deep_sz (l
 // d_dinv[i] = 1/((x_i - z)(x_i - zg)) over the LDE coset x_i = 3*w_N^i (launch before launch_deep)
 void launch_deep_denoms(const fe* d_roots, size_t Ntab, size_t N, fe z, fe zg, fe* d_dinv, hipStream_t s);
 void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p,
-                 const ProofConsts* dK, const fe* d_dinv /* from launch_deep_denoms */, fe* d_out, hipStream_t s,
+                 const DerivedConsts* dD, const fe* d_dinv /* from launch_deep_denoms */, fe* d_out, hipStream_t s,
                  int split = 0);
 void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s);
 // alpha read from device memory (written by launch_fri_coin)

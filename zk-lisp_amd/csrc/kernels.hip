@@ -31,18 +31,14 @@ void upload_alphas_from_device(ProofConsts* dK, const fe* d, int n, hipStream_t 
   if (n > 1024) throw std::invalid_argument("more than 1024 transition constraints");
   ZKL_HIPCHECK(hipMemcpyAsync(dK->alpha, d, sizeof(fe) * n, hipMemcpyDeviceToDevice, s));
 }
-void upload_deep_coeffs(ProofConsts* dK, const fe* h, int n, hipStream_t s) {
-  // deep_kernel's unreduced 64-bit digit columns stay below the 2^62 REDC bound for at most 256
-  // terms (column 3 takes four 26 x 26-bit products per term, < 2^54)
-  if (n > 256) throw std::invalid_argument("more than 256 DEEP coefficients (W + C)");
-  ZKL_HIPCHECK(hipMemcpyAsync(dK->deep, h, sizeof(fe) * n, hipMemcpyHostToDevice, s));
-  static thread_local std::vector<uint32_t> m;
-  m.assign((size_t)n * 5, 0);
-  const fe R = fe_pow64(fe{2, 0}, 156);
-  for (int i = 0; i < n; i++) limbs26(fe_mul(h[i], R), &m[(size_t)i * 5]);
-  ZKL_HIPCHECK(hipMemcpyAsync(dK->deep_m, m.data(), m.size() * 4, hipMemcpyHostToDevice, s));
-  ZKL_HIPCHECK(hipStreamSynchronize(s));  // m is reused by the next proof on this thread
+__global__ void pose_k_kernel(const ProofConsts* K, DerivedConsts* D) {
+  const int j = (int)threadIdx.x;
+  if (j >= 27) return;
+  uint32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 12; i++) mul_acc(K->alpha[12 * j + i], K->air.pose_rc[j][i], acc);
+  D->pose_k[j] = reduce288(acc);
 }
+void launch_pose_k(const ProofConsts* dK, DerivedConsts* dD, hipStream_t s) { pose_k_kernel<<<1, 64, 0, s>>>(dK, dD); }
 
 // =====================================================================================
 // NTT: in-place radix-2 passes, up to 8 stages per pass staged through LDS.
@@ -704,11 +700,15 @@ void launch_scale_bitrev(fe* d, size_t ncols, size_t n, const fe* scale, hipStre
 #else
 #define CE_OCC
 #endif
-template <bool POSE, bool RM>
+// PART 0: the whole transition sum; PART 2: all but the PoseidonAir block, whose sum pose_part[i]
+// (constraint_eval_pose_part_kernel) is added; PART 1: that block alone, written to out[i]
+template <bool POSE, bool RM, int PART = 0>
 __device__ __forceinline__ void constraint_eval_body(const fe* __restrict__ lde, const fe* __restrict__ roots,
                                                      int roots_shift, const fe* __restrict__ pertab,
                                                      const fe* __restrict__ bm, const ProofConsts* __restrict__ K,
-                                                     const fe* __restrict__ xinv, fe* __restrict__ out, int split) {
+                                                     const DerivedConsts* __restrict__ D, const fe* __restrict__ xinv,
+                                                     fe* __restrict__ out, int split,
+                                                     const fe* __restrict__ pose_part = nullptr) {
   const AirDevice& c_air = K->air;
   const CeParams& c_ce = K->ce;
   const size_t ce = c_ce.ce, N = c_ce.N;
@@ -730,13 +730,18 @@ __device__ __forceinline__ void constraint_eval_body(const fe* __restrict__ lde,
   fe x = fe_mul(fe{3, 0}, roots[i << roots_shift]);
   const size_t per_period = ce / (c_ce.n / 32);
   const fe* per = pertab + (i % per_period) * 31;
+  if (PART == 1) {
+    out[i] = air_transition_sum<POSE, RM, 1>(c_air, cur, nxt, per, fe_zero(), K->alpha, D->pose_k);
+    return;
+  }
   const size_t blow = ce / c_ce.n;
   const fe xn_inv = c_ce.xn_inv[i % blow];
   // p_last = L_{n-1}(x) = g^(n-1)/n * (x^n - 1) / (x - g^(n-1))
   fe x_gl = fe_sub_sel(x, c_ce.gl);
   fe xn_m1 = c_ce.xn_m1[i % blow];
   fe p_last = fe_mul(fe_mul(c_ce.lagr, xn_m1), xinv[i]);  // xinv[i] = 1 / (x - g^(n-1))
-  const fe tsum = air_transition_sum<POSE, RM>(c_air, cur, nxt, per, p_last, K->alpha);
+  fe tsum = air_transition_sum<POSE, RM, PART>(c_air, cur, nxt, per, p_last, K->alpha, D->pose_k);
+  if (PART == 2) tsum = fe_add(tsum, pose_part[i]);
   // boundary: sum_c P_c(x) M_c(x) - W(x)
   uint32_t bacc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint32_t nb = c_ce.n_bcols;
@@ -747,33 +752,50 @@ __device__ __forceinline__ void constraint_eval_body(const fe* __restrict__ lde,
 }
 
 // The VM-only and RAM / Merkle instances run at CE_WAVES_CFG waves per SIMD; the Poseidon
-// instances (90+ spilled VGPRs at 3 waves) keep the compiler's occupancy.
+// instances (90+ spilled VGPRs at 3 waves) run at CE_POSE_WAVES_CFG.
+#ifndef CE_POSE_WAVES_CFG
+#define CE_POSE_WAVES_CFG 0
+#endif
+#if CE_POSE_WAVES_CFG
+#define CE_POSE_OCC __attribute__((amdgpu_waves_per_eu(CE_POSE_WAVES_CFG, CE_POSE_WAVES_CFG)))
+#else
+#define CE_POSE_OCC
+#endif
 template <bool RM>
 __global__ __launch_bounds__(256) CE_OCC void constraint_eval_kernel(const fe* __restrict__ lde, const fe* __restrict__ roots,
                                                                     int roots_shift, const fe* __restrict__ pertab,
                                                                     const fe* __restrict__ bm,
                                                                     const ProofConsts* __restrict__ K,
+                                                                    const DerivedConsts* __restrict__ D,
                                                                     const fe* __restrict__ xinv, fe* __restrict__ out,
                                                                     int split) {
-  constraint_eval_body<false, RM>(lde, roots, roots_shift, pertab, bm, K, xinv, out, split);
+  constraint_eval_body<false, RM>(lde, roots, roots_shift, pertab, bm, K, D, xinv, out, split);
+}
+// Poseidon layouts in two kernels: the PoseidonAir block's alpha-weighted sum per CE point
+// (pose_part), then every other block plus that sum, at the VM-only kernel's occupancy.  One
+// kernel for both needed 256+ VGPRs (1 wave per SIMD).
+__global__ __launch_bounds__(256) CE_POSE_OCC void constraint_eval_pose_part_kernel(
+    const fe* __restrict__ lde, const fe* __restrict__ roots, int roots_shift, const fe* __restrict__ pertab,
+    const fe* __restrict__ bm, const ProofConsts* __restrict__ K, const DerivedConsts* __restrict__ D,
+    const fe* __restrict__ xinv, fe* __restrict__ pose_part, int split) {
+  constraint_eval_body<true, false, 1>(lde, roots, roots_shift, pertab, bm, K, D, xinv, pose_part, split);
 }
 template <bool RM>
-__global__ __launch_bounds__(256) void constraint_eval_pose_kernel(const fe* __restrict__ lde, const fe* __restrict__ roots,
+__global__ __launch_bounds__(256) CE_OCC void constraint_eval_pose_kernel(const fe* __restrict__ lde, const fe* __restrict__ roots,
                                                                   int roots_shift, const fe* __restrict__ pertab,
                                                                   const fe* __restrict__ bm,
                                                                   const ProofConsts* __restrict__ K,
+                                                                  const DerivedConsts* __restrict__ D,
                                                                   const fe* __restrict__ xinv, fe* __restrict__ out,
-                                                                  int split) {
-  constraint_eval_body<true, RM>(lde, roots, roots_shift, pertab, bm, K, xinv, out, split);
+                                                                  int split, const fe* __restrict__ pose_part) {
+  constraint_eval_body<true, RM, 2>(lde, roots, roots_shift, pertab, bm, K, D, xinv, out, split, pose_part);
 }
 
 // out[i] = 1 / ((x_i - a1) (x_i - a2)^two) over the coset x_i = 3 w_M^i (w_M^i =
 // roots[i << shift]): each thread inverts INV_PTS points T apart with one field inversion
 // (Montgomery's trick), instead of one ~250-multiplication Fermat inversion per point.  The
-// denominators are recomputed on the way back instead of kept: with both arrays live across the
-// inversion the compiler placed them in scratch (528 B per lane), and a kernel that needs scratch
-// makes the runtime allocate (and may reclaim) the queue's scratch between proofs.  The prefix
-// products go to the output slots instead (each slot k > 0 holds prefix k-1 until it is overwritten
+// prefix products are not kept in a private array (with the denominators, both live across the
+// inversion, the compiler placed them in scratch: 528 B per lane); they go to the output slots (each slot k > 0 holds prefix k-1 until it is overwritten
 // with its inverse on the way back): 32 extra bytes per point of HBM traffic, no private array.
 constexpr int INV_PTS = 16;
 __device__ inline fe coset_den(const fe* __restrict__ roots, size_t i, int shift, fe a1, fe a2, int two) {
@@ -806,21 +828,29 @@ static void launch_coset_inv(const fe* d_roots, int shift, size_t M, fe a1, fe a
 }
 
 void launch_constraint_eval(const fe* d_lde, const fe* d_roots, size_t Ntab, const fe* d_pertab, const fe* d_bm,
-                            const CeParams& p, ProofConsts* dK, bool pose_block, bool ram_merkle, fe* d_xinv,
-                            bool xinv_ready, fe* d_out, hipStream_t s, int split) {
+                            const CeParams& p, ProofConsts* dK, const DerivedConsts* dD, bool pose_block,
+                            bool ram_merkle, fe* d_xinv,
+                            bool xinv_ready, fe* d_out, hipStream_t s, int split, fe* d_pose_part) {
   ZKL_HIPCHECK(hipMemcpyAsync(&dK->ce, &p, sizeof p, hipMemcpyHostToDevice, s));
   int shift = ilog2s(Ntab) - ilog2s(p.ce);
   // 1 / (x - g^(n-1)) over the CE coset depends on the shape only: the caller keeps it per context
   if (!xinv_ready) launch_coset_inv(d_roots, shift, p.ce, p.gl, fe_zero(), 0, d_xinv, s);
   const unsigned grid = (unsigned)((p.ce + 255) / 256);
+  if (pose_block) {
+    if (!d_pose_part) throw std::invalid_argument("constraint evaluation: Poseidon layout needs the pose_part buffer");
+    constraint_eval_pose_part_kernel<<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, dD, d_xinv,
+                                                           d_pose_part, split);
+  }
   if (pose_block && ram_merkle)
-    constraint_eval_pose_kernel<true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
+    constraint_eval_pose_kernel<true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, dD, d_xinv, d_out,
+                                                           split, d_pose_part);
   else if (pose_block)
-    constraint_eval_pose_kernel<false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
+    constraint_eval_pose_kernel<false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, dD, d_xinv, d_out,
+                                                            split, d_pose_part);
   else if (ram_merkle)
-    constraint_eval_kernel<true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
+    constraint_eval_kernel<true><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, dD, d_xinv, d_out, split);
   else
-    constraint_eval_kernel<false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, d_xinv, d_out, split);
+    constraint_eval_kernel<false><<<grid, 256, 0, s>>>(d_lde, d_roots, shift, d_pertab, d_bm, dK, dD, d_xinv, d_out, split);
 }
 
 __global__ void boundary_scatter_kernel(const uint32_t* slot, const uint32_t* step, const fe* beta, size_t na, size_t n,
@@ -911,7 +941,7 @@ __device__ __forceinline__ fe limbs_canon(const uint32_t l[5]) {
 
 __global__ __launch_bounds__(256) void deep_kernel(const fe* __restrict__ lde, const fe* __restrict__ clde,
                                                    const fe* __restrict__ roots, int shift, DeepParams p,
-                                                   const ProofConsts* __restrict__ K, const fe* __restrict__ dinv,
+                                                   const DerivedConsts* __restrict__ K, const fe* __restrict__ dinv,
                                                    fe* out, int split) {
   const size_t T = (size_t)gridDim.x * blockDim.x;
   const size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -964,7 +994,7 @@ __global__ __launch_bounds__(256) void deep_kernel(const fe* __restrict__ lde, c
 // One block: thread i < W + C stores coefficient i and its Montgomery limbs; both frame dot
 // products are summed by a tree reduction in LDS.
 __global__ __launch_bounds__(256) void deep_coeffs_kernel(const fe* __restrict__ gam, uint32_t W, uint32_t C,
-                                                          const fe* __restrict__ frame, fe R156, ProofConsts* K) {
+                                                          const fe* __restrict__ frame, fe R156, DerivedConsts* K) {
   __shared__ fe red[2][256];
   const uint32_t i = threadIdx.x, n = W + C;
   fe a = fe_zero(), b = fe_zero();
@@ -993,7 +1023,7 @@ __global__ __launch_bounds__(256) void deep_coeffs_kernel(const fe* __restrict__
     K->deep_sz[1] = red[1][0];
   }
 }
-void launch_deep_coeffs(const fe* d_gam, uint32_t W, uint32_t C, const fe* d_frame, ProofConsts* dK, hipStream_t s) {
+void launch_deep_coeffs(const fe* d_gam, uint32_t W, uint32_t C, const fe* d_frame, DerivedConsts* dK, hipStream_t s) {
   if (W + C > 256) throw std::invalid_argument("more than 256 DEEP coefficients (W + C)");
   deep_coeffs_kernel<<<1, 256, 0, s>>>(d_gam, W, C, d_frame, fe_pow64(fe{2, 0}, 156), dK);
 }
@@ -1027,7 +1057,7 @@ void launch_deep_denoms(const fe* d_roots, size_t Ntab, size_t N, fe z, fe zg, f
 }
 
 void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Ntab, const DeepParams& p,
-                 const ProofConsts* dK, const fe* d_dinv, fe* d_out, hipStream_t s, int split) {
+                 const DerivedConsts* dK, const fe* d_dinv, fe* d_out, hipStream_t s, int split) {
   // N is a power of two >= 64: every thread gets exactly DEEP_PTS points
   const size_t threads = std::min<size_t>(256, p.N / DEEP_PTS);
   deep_kernel<<<(unsigned)(p.N / (threads * DEEP_PTS)), (unsigned)threads, 0, s>>>(

@@ -4,6 +4,7 @@
 // host keeps the Fiat-Shamir transcript (a few dozen permutations), builds Merkle
 // multiproof index sets and serialises Proof::to_bytes().
 #include <hip/hip_runtime.h>
+#include <malloc.h>
 #include <string.h>
 
 #include <atomic>
@@ -100,10 +101,12 @@ struct zkl_ctx {
   DBuf trace, coef, lde, parts, tree, ce, bvec, bm, clde, ctree, deep, draws, pw, oodv, oodf, txs, asl, ast, asv, ars;
   DBuf fri_ev, fri_tree, best, gaddr, gout, flag;
   DBuf xinv;    // batch-inverted coset denominators of DEEP (z-dependent)
+  DBuf posep;   // PoseidonAir block's share of the transition sum per CE point (Poseidon layouts)
   DBuf cexinv;  // 1 / (x - g^(n-1)) over the CE coset: shape-only, kept while the key matches
   size_t cexinv_key_n = 0, cexinv_key_ce = 0, cexinv_key_tab = 0;
   const void* cexinv_key_roots = nullptr;
-  DBuf kconst;  // ProofConsts of the proof in flight on this context
+  DBuf kconst;  // ProofConsts of the proof in flight on this context (written by copies only)
+  DBuf dconst;  // DerivedConsts: what the device derives per proof (pose_k, DEEP coefficients)
   DBuf fri_coin;  // device transcript of the FRI layers: seed, alpha, layer roots
   HBuf h_asrt, h_ood, h_addr, h_gv, h_tx, h_air;  // pinned staging: assertions, OOD frame, gather plan/values, transcript
   hipStream_t aux = nullptr;         // copy stream: assertion upload overlapped with the trace commitment
@@ -526,6 +529,8 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   const int Cc = air.num_comp_cols;
   C->kconst.ensure(sizeof(ProofConsts));
   ProofConsts* dK = (ProofConsts*)C->kconst.p;
+  C->dconst.ensure(sizeof(DerivedConsts));
+  DerivedConsts* dD = (DerivedConsts*)C->dconst.p;
   C->h_air.ensure(sizeof(AirDevice));
   memcpy(C->h_air.p, &air.dev, sizeof(AirDevice));
   upload_air_consts(dK, *C->h_air.at<AirDevice>(), s);
@@ -581,6 +586,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   check_launch("composition coefficient draws");
   coin.counter += ndraw;
   upload_alphas_from_device(dK, C->draws.f(), air.n_tc, s);
+  if (air.dev.pose_block) launch_pose_k(dK, dD, s);
 
   HIPCHECK(hipMemsetAsync(C->bvec.p, 0, (size_t)(nb + 1) * n * sizeof(fe), s));
   const fe* betas = C->draws.f() + air.n_tc;
@@ -630,8 +636,10 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
       C->cexinv_key_n = 0;  // invalid until the launch below has been queued
       C->cexinv.ensure(ce * sizeof(fe));
     }
-    launch_constraint_eval(C->lde.f(), roots, Ntab, C->pertab.f(), C->bm.f(), cp, dK, air.dev.pose_block != 0,
-                           (air.dev.ram_block | air.dev.merkle_block) != 0, C->cexinv.f(), ready, C->ce.f(), s, split);
+    if (air.dev.pose_block) C->posep.ensure(ce * sizeof(fe));
+    launch_constraint_eval(C->lde.f(), roots, Ntab, C->pertab.f(), C->bm.f(), cp, dK, dD, air.dev.pose_block != 0,
+                           (air.dev.ram_block | air.dev.merkle_block) != 0, C->cexinv.f(), ready, C->ce.f(), s, split,
+                           air.dev.pose_block ? C->posep.f() : nullptr);
     C->cexinv_key_n = n; C->cexinv_key_ce = ce; C->cexinv_key_tab = Ntab; C->cexinv_key_roots = roots;
   }
   check_launch("constraint evaluation");
@@ -740,7 +748,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   launch_draws(coin.seed, coin.counter, W + Cc, C->draws.f(), s);
   check_launch("DEEP coefficient draws");
   coin.counter += W + Cc;
-  launch_deep_coeffs(C->draws.f(), W, (uint32_t)Cc, dframe, dK, s);
+  launch_deep_coeffs(C->draws.f(), W, (uint32_t)Cc, dframe, dD, s);
   check_launch("DEEP coefficients");
   HT("gam");
   DeepParams dp{};
@@ -748,7 +756,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   C->deep.ensure(N * sizeof(fe));
   {
     KScope k(C, KF_DEEP);
-    launch_deep(C->lde.f(), C->clde.f(), roots, Ntab, dp, dK, C->xinv.f(), C->deep.f(), s, split);
+    launch_deep(C->lde.f(), C->clde.f(), roots, Ntab, dp, dD, C->xinv.f(), C->deep.f(), s, split);
   }
   check_launch("DEEP composition");
   T.mark(6);
@@ -1057,6 +1065,21 @@ int zkl_hip_init(int device, zkl_ctx** out) {
         const char* e = getenv("ZKL_SPIN");
         if (!(e && !strcmp(e, "0"))) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
         (void)hipGetLastError();
+        // Host memory handed back to the kernel (munmap, heap trim) while a proof runs was
+        // followed by 10-30 ms of idle GPU in ~1 proof of 3 (the driver updates the process's GPU
+        // mappings and stops its queues meanwhile).  glibc returns memory on
+        // free() of blocks above its (dynamic) mmap threshold and when the free heap top
+        // exceeds the trim threshold, so the process keeps what it allocated instead: blocks
+        // below 32 MiB (glibc's largest mmap threshold) come from the heap, the heap grows in
+        // 64 MiB steps and is not trimmed until 2 GiB of its top are free.  Measured: 3 of 3
+        // processes with stalled proofs under glibc's defaults, 0 of 3 with the heap kept
+        // (profiles/r04/stalls.md).  ZKL_MALLOC_TUNE=0 keeps glibc's defaults.
+        const char* m = getenv("ZKL_MALLOC_TUNE");
+        if (!(m && !strcmp(m, "0"))) {
+          (void)mallopt(M_MMAP_THRESHOLD, 32 << 20);
+          (void)mallopt(M_TOP_PAD, 64 << 20);
+          (void)mallopt(M_TRIM_THRESHOLD, 0x7fffffff);
+        }
       });
     }
     auto* c = new zkl_ctx();
