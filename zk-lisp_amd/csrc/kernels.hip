@@ -1099,6 +1099,7 @@ void launch_gather(const uint64_t* d_addrs, size_t k, fe* d_out, hipStream_t s) 
 namespace zkl {
 const char* kernels_build_config() {
   return "NTT_ELEMS=" ZKL_STR(NTT_ELEMS_CFG) ";NTT_THREADS=" ZKL_STR(NTT_THREADS_CFG) ";CE_WAVES=" ZKL_STR(
-      CE_WAVES_CFG) ";DEEP_PTS=" ZKL_STR(DEEP_PTS_CFG) ";DEEP_COLS=" ZKL_STR(DEEP_COLS_CFG);
+      CE_WAVES_CFG) ";CE_POSE_WAVES=" ZKL_STR(CE_POSE_WAVES_CFG) ";DEEP_PTS=" ZKL_STR(DEEP_PTS_CFG) ";DEEP_COLS=" ZKL_STR(
+      DEEP_COLS_CFG);
 }
 }  // namespace zkl
