@@ -51,7 +51,7 @@ SEED0 = 0x5EED0001             # segment seed of rank / segment 0 (SURVEY §8(d)
 GOLDEN = os.path.join(ROOT, "tests", "golden", "proof_2p16.json")
 CHAIN = os.path.join(ROOT, "tests", "golden", "chain_2p16.json")  # the multi-segment program (make_chain_goldens.py)
 PROGRAMS = os.path.join(ROOT, "tests", "golden", "programs.json")  # real .zlisp programs (make_programs.py)
-VALU_MIX = os.path.join(ROOT, "profiles", "r02", "valu_mix.json")
+VALU_MIX = os.path.join(ROOT, "profiles", "r04", "valu_mix.json")
 VALU_FLOOR = os.path.join(ROOT, "profiles", "r03", "valu_floor.json")
 ROW_KERNEL = {"mfma": "hash_rows_pm_kernel<0>", "lane": "hash_rows_kernel<0>"}
 
@@ -230,7 +230,7 @@ def cpu_baseline(log_n, threads, gpu_proof, log_n_target):
 
 def valu_roofline(perms_per_s):
     """Achieved permutations/s of the row hash against the ceiling its own instruction mix
-    implies at the measured per-class VALU rates (tools/valu_mix.py -> profiles/r02/valu_mix.json)."""
+    implies at the measured per-class VALU rates (tools/valu_mix.py -> profiles/r04/valu_mix.json)."""
     try:
         mix = json.load(open(VALU_MIX))
     except (OSError, ValueError):
