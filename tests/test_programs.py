@@ -87,6 +87,19 @@ def test_op_list_and_program_id_from_source(name, oracle):
     assert ([list(a) for a in schema[0]], schema[1]) == tuple(g["schema"])
 
 
+@have_ref
+def test_fib_2pow16_is_256_segments_not_one():
+    """BASELINE configs[1] names examples/fib-2pow16.zlisp as "1 segment, 65536 rows": the
+    program's loop of 2^16 iterations lowers to 458,751 ops, i.e. 2^19 levels = 2^24 rows, which
+    the segment planner cuts into 256 segments of 65,536 rows."""
+    import lower_ref
+    src = open(os.path.join(EXAMPLES, "fib-2pow16.zlisp")).read()
+    ops = lower_ref.compile_entry(src, [])[0]
+    assert len(ops) == 458751 and ops[-1][0] == "End"
+    plan = zkl_hip.plan_segments(len(ops), 1 << 16)
+    assert len(plan) == 256 and all(b - a == 1 << 16 for a, b in plan)
+
+
 def test_rollup_op_list_shape():
     """rollup-bench lowers to 1,791 ops: 2,048 levels (65,536 rows), the published run's 16 x
     4096; its RAM traffic is the 8 + 64 table stores, the 15 applied transfers (loop bodies run
