@@ -20,8 +20,9 @@ Moves, selects and address arithmetic are free in every option (as in the floor)
      Toeplitz rows (shifted digit copies, 256 bytes per state) are built by byte permutes.  The
      31 output columns then still need the carry + REDC the VALU does today.
   C  no final REDC: the unreduced x^2 * x (260 bits, 10 columns) carried into 33 offset bytes
-     and fed to the MDS MFMA against digits of M * 2^(8j) mod p for j < 33 (13 k-steps per tile
-     instead of 7).  Saves one REDC130 but needs a 9-step column carry and twice the packing.
+     and fed to the MDS MFMA against digits of M * 2^(8j) / R' mod p for j < 33 (13 k-steps per
+     tile instead of 7).  Saves one REDC130 but needs a 9-step column carry, twice the packing,
+     and an unpaired digit-column fold (the column sums grow to 2^24).
   D  f64 FMA limbs: 6 x 24-bit limbs (products < 2^48, column sums of <= 6 exact in 53 bits),
      36 v_fma_f64 per product; the REDC steps also in f64 (floor / fma splitting per digit).
   E  24-bit integer products: 6 x 24-bit limbs, each 48-bit product as v_mad_u32_u24 (low 32)
@@ -90,7 +91,10 @@ def options():
                     pack16),
          "mfma_per_wave_round": 42 + B_mfma}
     # C: carry 10 columns into 26-bit limbs (9 x (and, 64-bit shift+add)), pack 33 bytes (~2x pack)
-    C = {"ops": add({"mad": 15, "alu32": 4}, {"mad": 25}, redc130(), {"alu64": 9, "alu32": 9}, fold, {"alu32": 26}),
+    # the digit-column sums then run over 12 x 33 bytes: |Y_c| < 2^24, so two neighbouring
+    # digits no longer pair in 32 bits and the fold takes 16 mads instead of 10
+    C = {"ops": add({"mad": 15, "alu32": 4}, {"mad": 25}, redc130(), {"alu64": 9, "alu32": 9}, fold, {"mad": 6},
+                    {"alu32": 26}),
          "mfma_per_wave_round": 6 * 13}
     # D: 36 fma per product, 21 for the square (symmetric), REDC in f64: per 24-bit digit (6):
     # floor-split (2 fma), m*p contributions (3 fma), carry (2 fma) ~ 7
