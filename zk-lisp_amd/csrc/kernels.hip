@@ -751,10 +751,11 @@ __device__ __forceinline__ void constraint_eval_body(const fe* __restrict__ lde,
   out[i] = fe_mul(v, xn_inv);
 }
 
-// The VM-only and RAM / Merkle instances run at CE_WAVES_CFG waves per SIMD; the Poseidon
-// instances (90+ spilled VGPRs at 3 waves) run at CE_POSE_WAVES_CFG.
+// The VM-only and RAM / Merkle instances run at CE_WAVES_CFG waves per SIMD; the PoseidonAir
+// block's own kernel at CE_POSE_WAVES_CFG (3: 48 spilled VGPRs, 3.33 against 3.42 ms of
+// evaluation per rollup-bench proof at the compiler's 2, profiles/r04/ab_cepose.json).
 #ifndef CE_POSE_WAVES_CFG
-#define CE_POSE_WAVES_CFG 0
+#define CE_POSE_WAVES_CFG 3
 #endif
 #if CE_POSE_WAVES_CFG
 #define CE_POSE_OCC __attribute__((amdgpu_waves_per_eu(CE_POSE_WAVES_CFG, CE_POSE_WAVES_CFG)))
