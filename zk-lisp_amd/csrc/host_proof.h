@@ -65,9 +65,14 @@ struct Plan {
 inline Plan batch_plan(size_t n_leaves, const std::vector<size_t>& idx) {
   const int depth = ilog2(n_leaves);
   const size_t Q = idx.size();
-  // normalised leaf pairs (sorted, unique) and the requested leaves (sorted) in one scratch block
-  std::unique_ptr<size_t[]> buf(new size_t[2 * Q + 2]);
-  size_t* norm = buf.get();
+  // scratch kept per thread (one plan per tree and FRI layer of every proof: no allocation in
+  // the steady state)
+  static thread_local std::vector<size_t> sbuf, scur;
+  static thread_local std::vector<uint64_t> stmp;
+  static thread_local std::vector<uint32_t> scnt;
+  // normalised leaf pairs (sorted, unique) and the requested leaves (sorted)
+  sbuf.resize(2 * Q + 2);
+  size_t* norm = sbuf.data();
   size_t* req = norm + Q + 1;
   for (size_t k = 0; k < Q; k++) { norm[k] = idx[k] & ~(size_t)1; req[k] = idx[k]; }
   std::sort(norm, norm + Q);
@@ -75,10 +80,12 @@ inline Plan batch_plan(size_t n_leaves, const std::vector<size_t>& idx) {
   std::sort(req, req + Q);
   // list k takes at most two leaves and one node per level: fixed-stride scratch, compacted
   const size_t stride = (size_t)depth + 2;
-  std::unique_ptr<uint64_t[]> tmp(new uint64_t[L * stride]);
-  std::unique_ptr<uint32_t[]> cnt(new uint32_t[L]());
-  std::unique_ptr<size_t[]> cur_b(new size_t[2 * L + 2]);
-  size_t *cur = cur_b.get(), *nxt = cur + L + 1;
+  stmp.resize(L * stride);
+  scnt.assign(L, 0);
+  scur.resize(2 * L + 2);
+  uint64_t* tmp = stmp.data();
+  uint32_t* cnt = scnt.data();
+  size_t *cur = scur.data(), *nxt = cur + L + 1;
   for (size_t k = 0; k < L; k++) {
     for (size_t j = norm[k]; j < norm[k] + 2; j++)
       if (!std::binary_search(req, req + Q, j)) tmp[k * stride + cnt[k]++] = n_leaves + j;
@@ -97,13 +104,13 @@ inline Plan batch_plan(size_t n_leaves, const std::vector<size_t>& idx) {
     nc = nn;
   }
   Plan P;
-  P.len.assign(cnt.get(), cnt.get() + L);
+  P.len.assign(cnt, cnt + L);
   size_t tot = 0;
   for (size_t k = 0; k < L; k++) tot += cnt[k];
   P.node.resize(tot);
   size_t o = 0;
   for (size_t k = 0; k < L; k++) {
-    memcpy(P.node.data() + o, tmp.get() + k * stride, cnt[k] * sizeof(uint64_t));
+    memcpy(P.node.data() + o, tmp + k * stride, cnt[k] * sizeof(uint64_t));
     o += cnt[k];
   }
   return P;
