@@ -776,6 +776,8 @@ def main():
             "stage_ms_untimed_step": {k: round(v, 3) for k, v in stages.items()},
             "host_ms_last_step": {k: round(v, 3) for k, v in host.items()},
             "call_ms_each_step": [round(v, 2) for v in step_ms],
+            # stalled-step check: slowest step over the median step
+            "max_over_median_step": round(max(step_ms) / sorted(step_ms)[len(step_ms) // 2], 3) if step_ms else None,
             **({"stage_ms_each_step": step_stages} if step_stages else {}),
             "step_handoff": hand,
         }
