@@ -51,6 +51,7 @@ SEED0 = 0x5EED0001             # segment seed of rank / segment 0 (SURVEY §8(d)
 GOLDEN = os.path.join(ROOT, "tests", "golden", "proof_2p16.json")
 CHAIN = os.path.join(ROOT, "tests", "golden", "chain_2p16.json")  # the multi-segment program (make_chain_goldens.py)
 PROGRAMS = os.path.join(ROOT, "tests", "golden", "programs.json")  # real .zlisp programs (make_programs.py)
+FIB = os.path.join(ROOT, "tests", "golden", "fib_2pow16.json")  # examples/fib-2pow16.zlisp (make_fib_2pow16.py)
 VALU_MIX = os.path.join(ROOT, "profiles", "r04", "valu_mix.json")
 VALU_FLOOR = os.path.join(ROOT, "profiles", "r03", "valu_floor.json")
 ROW_KERNEL = {"mfma": "hash_rows_pm_kernel<0>", "lane": "hash_rows_kernel<0>"}
@@ -307,11 +308,18 @@ def lines_for_rank(args, world):
         lines.append("c4_sharded")
     if args.c5_log_n > 0:
         lines.append("c5_single_segment")
+    lines += [f"program:{p}" for p in program_specs(args)]
     if world == 1:
         lines += [x for x, on in (("host_trace", args.host_steps > 0), ("c3_in_gpu_pipeline", args.c3_segments > 0),
                                   ("real_program", args.program_steps > 0),
                                   ("cpu_baseline", not args.no_cpu_baseline)) if on]
     return lines
+
+
+def program_specs(args):
+    if args.programs in ("", "none"):
+        return []
+    return [p for p in args.programs.split(",") if p]
 
 
 # ------------------------------------------------------------------------ workloads
@@ -406,6 +414,164 @@ def real_program(zkl_hip, device, steps, name="rollup-bench", max_rows=1 << 16):
             "kernel_ms_per_family_untimed_step": fam}
 
 
+def load_program(zkl_hip, name):
+    """(ops, program_id, secret u64 args, main args, max_rows -> {segment index: golden}) of a real
+    example: rollup-bench / fib-2pow16-log-n from tests/golden/programs.json, fib-2pow16 from
+    tests/golden/fib_2pow16.json and its gzip'd op list (the compiler's output, committed as data)."""
+    if name == "fib-2pow16":
+        import gzip
+        g = json.load(open(FIB))
+        raw = gzip.open(os.path.join(os.path.dirname(FIB), g["ops_file"])).read()
+        if hashlib.sha256(raw).hexdigest() != g["ops_json_sha256"]:
+            raise RuntimeError("fib-2pow16 op list fixture does not match its sha256")
+        ops = [zkl_hip.op(k, **f) for k, f in json.loads(raw)]
+        gold = {g["max_segment_rows"]: {int(k): v for k, v in g["segments"].items()}}
+        return ops, bytes.fromhex(g["program_id"]), [], [], gold
+    tab = json.load(open(PROGRAMS))[name]
+    ops = [zkl_hip.op(k, **f) for k, f in tab["ops"]]
+    main_args = [(tg, bytes.fromhex(b)) for tg, b in tab["cli"]["main_args"]]
+    gold = {int(mr): dict(enumerate(p["segments"])) for mr, p in tab["plans"].items()}
+    aggs = {int(mr): p.get("aggregation", {}) for mr, p in tab["plans"].items()}
+    return ops, bytes.fromhex(tab["program_id"]), tab["cli"]["secret_u64"], main_args, gold, aggs
+
+
+def program_sharded(zkl_hip, dist, device, rank, world, name, max_rows, inflight, builders, resident=False):
+    """`zk-lisp prove examples/<name>.zlisp --max-segment-rows <max_rows>` sharded over the ranks
+    (segment i on rank i mod N, prove.rs:1018-1050's pool per rank): each rank runs the program
+    once (zkl_program_new), builds only its own segments (zkl_build_segment_trace, no full trace)
+    on `builders` host threads straight into pinned trace buffers and proves them through the
+    host-trace entry point with `inflight` contexts (zkl_hip.program.prove_program) -- timed end
+    to end between barriers, value = segments / max-over-ranks seconds.  Then the zl1 steps go to
+    rank 0 over RCCL, which checks the VM-state chain and proves the aggregation.  At N = 1 with
+    `resident`, the same segments are also proved from HBM-resident traces (the headline's
+    definition: trace already on the device).  A failing rank still passes every barrier and
+    collective (the error flag is reduced over the ranks first), so no rank is left waiting."""
+    from zkl_hip.program import prove_program, steps_of
+    err, ctxs, P, plan, dt, par, res_line, enc = None, [], None, [], 0.0, [], None, []
+    build_ms = prove_ms = [0.0]
+    run_s = 0.0
+    aggs = {}
+    try:
+        loaded = load_program(zkl_hip, name)
+        ops, pid, secret, main_args, gold = loaded[:5]
+        aggs = loaded[5] if len(loaded) > 5 else {}
+        t_run = time.perf_counter()
+        P = zkl_hip.Program(ops, pid, secret_args=secret, main_args=main_args)
+        run_s = time.perf_counter() - t_run
+        plan = zkl_hip.plan_segments(len(ops), max_rows)
+        mine = dist.segments_for_rank(len(plan), rank, world)
+        ctxs = [zkl_hip.Context(device) for _ in range(inflight)]
+        prove_program(P, plan, segments=mine[:inflight], contexts=ctxs, builders=builders)  # warm contexts
+    except Exception as e:  # noqa: BLE001
+        err = f"setup: {e}"
+    dist.barrier()
+    if err is None:
+        try:
+            t0 = time.perf_counter()
+            recs = prove_program(P, plan, segments=mine, contexts=ctxs, builders=builders)
+            dt = time.perf_counter() - t0
+            g = gold.get(max_rows, {})
+            par = [("match" if hashlib.sha256(r.proof).hexdigest() == g[i]["proof_sha256"] else "MISMATCH")
+                   for i, r in recs.items() if i in g]
+            build_ms = sorted(r.build_ms for r in recs.values())
+            prove_ms = sorted(r.prove_ms for r in recs.values())
+            enc = steps_of(list(recs.values()), len(plan), main_args=main_args)
+        except Exception as e:  # noqa: BLE001
+            err = f"prove: {e}"
+    dist.barrier()
+    el = dist.max_over_ranks(dt)
+    failed = dist.max_over_ranks(1.0 if err else 0.0) > 0
+    par_all = dist.gather_to_root(par)
+    errs = [e for e in (dist.gather_to_root(err) or []) if e]
+    if not failed and resident and world == 1:
+        try:
+            res_line = program_resident(zkl_hip, ctxs, P, plan, mine, builders)
+        except Exception as e:  # noqa: BLE001
+            res_line = {"error": str(e)}
+    for c in ctxs:
+        c.close()
+    if failed:
+        return {"error": "; ".join(f"rank {i}: {e}" for i, e in enumerate(errs))} if rank == 0 else None
+    comm, cerr = dist.init_rccl(device)
+    t_h = time.perf_counter()
+    steps = dist.collect_step_proofs(enc, comm)
+    if rank != 0:
+        return None
+    flat = [x for r in par_all for x in r]
+    widths = sorted({P.segment_width(a, b) for a, b in plan})
+    out = {"config": f"examples/{name}.zlisp --max-segment-rows {max_rows}: {len(plan)} segments of "
+                     f"{plan[0][1] - plan[0][0]} rows (widths {widths}), blowup 16, q 64, grind 16, sharded over "
+                     f"{world} rank(s), {inflight} contexts in flight per rank; traces built per segment "
+                     "(zkl_build_segment_trace) into pinned buffers and proved through zkl_hip_prove_segment",
+           "value": round(len(plan) / el, 4), "unit": "segment-proofs/s", "seconds": round(el, 3),
+           "segments": len(plan), "program_run_s": round(run_s, 2),
+           "build_ms_per_segment_median": round(build_ms[len(build_ms) // 2], 1),
+           "prove_call_ms_median": round(prove_ms[len(prove_ms) // 2], 1),
+           "golden_matches": flat.count("match"), "golden_mismatches": flat.count("MISMATCH"),
+           "handoff": {"ms": round((time.perf_counter() - t_h) * 1e3, 1),
+                       "transport": "rccl" if comm is not None else f"gloo ({cerr})",
+                       "step_bytes": sum(d["bytes"] for d in steps)}}
+    if res_line is not None:
+        out["resident"] = res_line
+    raw = [d["raw"] for d in steps]
+    try:
+        t1 = time.perf_counter()
+        art, dg = zkl_hip.agg_prove(raw)
+        a = {"children": len(raw), "ms": round((time.perf_counter() - t1) * 1e3, 1), "artifact_bytes": len(art)}
+        zkl_hip.agg_verify(art)
+        a["verified"] = True
+        want = aggs.get(max_rows, {}).get("valid")
+        if want:
+            a["golden"] = "match" if hashlib.sha256(art).hexdigest() == want["sha256"] else "MISMATCH"
+        out["aggregation"] = a
+    except Exception as e:  # reported in the line, and the run exits non-zero
+        out["aggregation"] = {"error": str(e)}
+    return out
+
+
+def program_resident(zkl_hip, ctxs, P, plan, idx, builders):
+    """The program's segments built on `builders` host threads, uploaded (all resident in HBM:
+    256 x 214 MB = 55 GB for fib-2pow16) and proved from HBM by the contexts in flight: the
+    headline's definition of a step (trace already on the device)."""
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+    inflight = len(ctxs)
+    segs = []
+    try:
+        win = 2 * max(1, builders)  # host traces alive at once
+        with ThreadPoolExecutor(max_workers=max(1, builders)) as ex:
+            futs = {k: ex.submit(P.segment, *plan[i]) for k, i in enumerate(idx[:win])}
+            for k in range(len(idx)):
+                t, pi, w, _, _ = futs.pop(k).result()
+                if k + win < len(idx):
+                    futs[k + win] = ex.submit(P.segment, *plan[idx[k + win]])
+                m = len(t) // w
+                c = ctxs[k % inflight]
+                d = c.alloc(w * m * 16)
+                c.upload(d, t, w * m * 16)
+                segs.append((c, d, pi, w, m, zkl_hip.proof_options(w, m)))
+                del t
+
+        def work(k):
+            for c, d, pi, w, m, o in segs[k::inflight]:
+                c.prove_segment_device(d, w, m, pi, o)
+
+        th = [threading.Thread(target=work, args=(k,)) for k in range(inflight)]
+        t0 = time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        for c in ctxs:
+            c.synchronize()
+        dt = time.perf_counter() - t0
+    finally:
+        for c, d, *_ in segs:
+            c.free(d)
+    return {"value": round(len(segs) / dt, 4), "unit": "segment-proofs/s", "seconds": round(dt, 3),
+            "note": "every segment's trace resident in HBM before the timed region; same contexts in flight"}
+
+
 class Pipeline:
     """A set of distinct segments resident in HBM, proved by `inflight` contexts (one HIP
     stream each) in host threads, so one segment's latency-bound tails (tree tops, FRI
@@ -495,6 +661,68 @@ def host_inflight(zkl_hip, device, trace, W, n, pi, opts, steps):
             "fraction_of_resident_rate": round(r_host / r_dev, 4)}
 
 
+def host_fresh(zkl_hip, device, trace, W, n, pi, opts, steps):
+    """The Rust binding's allocation pattern (prove.rs:1103-1142: a fresh TraceTable per segment,
+    filled, proved, dropped): two contexts in flight, each proof from a newly malloc'd host trace
+    (214 MB, filled with a copy of the trace, freed after its proof) -- against the same with the
+    contexts' pinned trace buffers (zkl_hip_trace_buffer, two slots, filled in place, nothing
+    allocated per proof).  Per-proof call times: median and slowest / median (stalled proofs,
+    DESIGN.md §6)."""
+    import ctypes as C
+    import threading
+    libc = C.CDLL("libc.so.6")
+    libc.malloc.restype = C.c_void_p
+    libc.malloc.argtypes = [C.c_size_t]
+    libc.free.argtypes = [C.c_void_p]
+    nbytes = W * n * 16
+    ctxs = [zkl_hip.Context(device) for _ in range(2)]
+    src = C.addressof(trace)
+    res = {}
+    try:
+        for c in ctxs:
+            c.prove_segment(trace, W, n, pi, opts)  # warm (buffers, tables, upload ring)
+
+        def run(mode):
+            times = [[] for _ in ctxs]
+            bufs = [[c.trace_buffer(nbytes, k) for k in (0, 1)] for c in ctxs] if mode == "pinned" else None
+
+            def work(k):
+                for j in range(steps):
+                    t0 = time.perf_counter()
+                    if mode == "pinned":
+                        p = bufs[k][j % 2]
+                    else:
+                        p = libc.malloc(nbytes)
+                        if not p:
+                            raise MemoryError("malloc of the host trace failed")
+                    C.memmove(p, src, nbytes)
+                    ctxs[k].prove_segment(p, W, n, pi, opts)
+                    if mode != "pinned":
+                        libc.free(p)
+                    times[k].append((time.perf_counter() - t0) * 1e3)
+            th = [threading.Thread(target=work, args=(k,)) for k in range(len(ctxs))]
+            t0 = time.perf_counter()
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            dt = time.perf_counter() - t0
+            flat = sorted(t for ts in times for t in ts)
+            med = flat[len(flat) // 2]
+            return {"value": round(len(flat) / dt, 4), "unit": "segment-proofs/s",
+                    "ms_per_proof_call_median": round(med, 2), "max_over_median": round(flat[-1] / med, 3),
+                    "ms_each": [[round(t, 1) for t in ts] for ts in times]}
+
+        res["fresh_malloc"] = run("fresh")
+        res["pinned_trace_buffer"] = run("pinned")
+    finally:
+        for c in ctxs:
+            c.close()
+    res["note"] = ("2 contexts in flight; each proof's time includes filling the host trace (a 214 MB copy) "
+                   "and its upload inside zkl_hip_prove_segment")
+    return res
+
+
 def step_info(zkl_hip, pi, index, total):
     """zl1 step metadata of segment `index` of `total`; the synthetic boundary chain is
     state_out(i) = state_in(i+1) = i+1 (what the aggregation checks)."""
@@ -552,6 +780,12 @@ def main():
                     help="proofs of the real rollup-bench.zlisp 65,536-row segment (N = 1; 0: skip)")
     ap.add_argument("--host-steps", type=int, default=5,
                     help="proofs timed through zkl_hip_prove_segment with a host-resident trace (N = 1; 0: skip)")
+    ap.add_argument("--programs", default="fib-2pow16:65536,rollup-bench:1024",
+                    help="real example programs proved segment by segment, sharded over the ranks "
+                         "(name:max_segment_rows,...; 'none' to skip)")
+    ap.add_argument("--program-inflight", type=int, default=4, help="contexts in flight per rank for --programs")
+    ap.add_argument("--tuning", default="spin,malloc",
+                    help="opt-in process settings this process applies (zkl_hip_process_tuning): spin, malloc, none")
     ap.add_argument("--dry-run", action="store_true", help="launcher / rank plumbing only, no device work (CPU tests)")
     args = ap.parse_args()
     if args.gpus < 1:
@@ -600,6 +834,8 @@ def main():
         log(f"bench: rank {rank} needs device {device} but {n_dev} HIP device(s) are visible "
             f"(set ZKL_BENCH_DEVICE to rehearse {world} ranks on fewer GPUs)")
         return 3
+    want = {x for x in args.tuning.split(",") if x and x != "none"}
+    tuning = zkl_hip.process_tuning(spin="spin" in want, malloc="malloc" in want)  # before the first context
     ctx = zkl_hip.Context(device)
     log_n = args.log_n
     n = 1 << log_n
@@ -657,11 +893,13 @@ def main():
         ctx.synchronize()
         dth = time.perf_counter() - t1
         inflight2 = host_inflight(zkl_hip, device, trace, W, n, pi, opts, args.host_steps)
+        fresh = host_fresh(zkl_hip, device, trace, W, n, pi, opts, max(4, args.host_steps))
         host_line = {"entry": "zkl_hip_prove_segment (trace in pageable host memory, uploaded inside each proof)",
                      "value": round(args.host_steps / dth, 4), "unit": "segment-proofs/s",
                      "ms_per_proof": round(dth / args.host_steps * 1e3, 3), "steps": args.host_steps,
                      "trace_bytes": nbytes, "upload_loop_ms_last_proof": round(ctx.host_times().get("upload", 0.0), 3),
-                     "parity": parity_of(hp, seed, log_n)["golden"], "two_contexts_in_flight": inflight2}
+                     "parity": parity_of(hp, seed, log_n)["golden"], "two_contexts_in_flight": inflight2,
+                     "per_proof_allocation": fresh}
     del trace
     ctx.close()
     hand, _ = handoff(zkl_hip, dist, [(rank, pi, proof)], world, device=device)
@@ -716,6 +954,16 @@ def main():
                       "value": round(world / (ms5 * 1e-3), 4), "unit": "segment-proofs/s",
                       "ms_per_proof": round(ms5, 1), "proof_bytes": pb5,
                       "rows_per_s": round(world * (1 << args.c5_log_n) / ms5 * 1e3)}
+
+    # real example programs, segment by segment, sharded over the ranks
+    prog_lines = {}
+    builders = max(2, cpu_threads(args.cpu_threads) // world)
+    for spec in program_specs(args):
+        name, mr = spec.split(":")
+        pl_out = program_sharded(zkl_hip, dist, device, rank, world, name, int(mr), args.program_inflight,
+                                 builders, resident=(name == "fib-2pow16"))
+        if rank == 0:
+            prog_lines[spec] = pl_out
 
     if rank == 0:
         value = world * args.steps / elapsed
@@ -821,6 +1069,13 @@ def main():
             out["c5_single_segment"] = c5
             if "error" in c5:
                 failures.append("c5_single_segment")
+        if prog_lines:
+            out["programs"] = prog_lines
+            for spec, pl_out in prog_lines.items():
+                if "error" in pl_out or pl_out.get("golden_mismatches") or "error" in pl_out.get("aggregation", {}) \
+                        or pl_out.get("aggregation", {}).get("golden") == "MISMATCH":
+                    failures.append(f"program {spec}")
+        out["process_tuning"] = tuning
         if world == 1 and args.program_steps > 0:
             try:
                 out["real_program"] = real_program(zkl_hip, device, args.program_steps)

@@ -130,6 +130,22 @@ int zkl_hip_abi_version(void);
  * parity-tested configuration (no timing probes are compiled in; tests/test_abi.py) */
 const char* zkl_hip_build_config(void);
 
+/* ---- process-level settings (opt-in) --------------------------------------------------
+ * zkl_hip_init changes nothing outside the library.  These process-wide settings helped the
+ * prover on some hosts and are the embedding application's choice:
+ *   ZKL_TUNE_SPIN    hipSetDeviceFlags(hipDeviceScheduleSpin) on every visible device: host waits
+ *                    on the device spin instead of sleeping (a blocking wait was seen to wake
+ *                    20-30 ms late); costs one host core per waiting context.  Takes effect only
+ *                    before the first zkl_hip_init / HIP context of the process.
+ *   ZKL_TUNE_MALLOC  glibc mallopt: mmap threshold 32 MiB, top pad 64 MiB, trim threshold 2 GiB --
+ *                    the process keeps freed heap memory instead of returning it to the kernel
+ *                    (memory returned while a proof ran was followed by idle GPU time).
+ *                    Changes the allocator of the whole host process.
+ * *applied receives the flags that took effect; ZKL_OK if all requested did. */
+#define ZKL_TUNE_SPIN 1u
+#define ZKL_TUNE_MALLOC 2u
+int zkl_hip_process_tuning(uint32_t flags, uint32_t* applied);
+
 /* ---- the drop-in: one segment proof ----------------------------------------
  * Replaces ZkProver::prove -> winterfell::Prover::prove (prove.rs:174-257) for
  * ZkLispAir + PoseidonHasher + MerkleTree + DefaultRandomCoin (prove.rs:425-437).
@@ -137,6 +153,17 @@ const char* zkl_hip_build_config(void);
 int zkl_hip_prove_segment(zkl_ctx* ctx, const zkl_f128* trace, uint32_t width, uint32_t n_rows,
                           const zkl_air_public_inputs* pi, const zkl_proof_options* opts,
                           uint8_t** proof_out, size_t* proof_len);
+
+/* Pinned host buffers owned by ctx for the next traces: slot 0 .. ZKL_TRACE_BUFFERS - 1, each at
+ * least `bytes` (grown when needed, kept across proofs, freed by zkl_hip_destroy).  The caller
+ * fills one -- zkl_build_segment_trace can write a segment straight into it -- and passes it as
+ * `trace` to zkl_hip_prove_segment, which then DMAs the columns from it with no staging copy and no
+ * per-proof host allocation on the caller's side (prove.rs:1103-1142 allocates a fresh TraceTable
+ * per segment and drops it after the proof).  Two slots let the next segment be built while the
+ * current one proves.  A slot must not be written while a proof reads it; valid until the next
+ * call that grows it. */
+#define ZKL_TRACE_BUFFERS 2
+int zkl_hip_trace_buffer(zkl_ctx* ctx, uint32_t slot, size_t bytes, zkl_f128** out);
 
 /* Same, with the trace already resident in HBM (device pointer on ctx's device,
  * column-major).  Used by the multi-segment pipeline and by bench.py. */
@@ -330,6 +357,26 @@ int zkl_plan_segments(uint32_t n_ops, uint32_t max_rows, uint32_t* r_starts, uin
 int zkl_slice_segment(const zkl_f128* full, uint32_t full_width, uint32_t n_full, const zkl_op* ops, uint32_t n_ops,
                       const zkl_air_public_inputs* pi_full, uint32_t r_start, uint32_t r_end, zkl_f128* trace_out,
                       zkl_air_public_inputs* pi_out, uint32_t* width_out, uint8_t state_in[32], uint8_t state_out[32]);
+
+/* Per-segment trace builder: what prove_segment's input side (prove.rs:1057-1134,
+ * build_segment_trace_with_state_without_full mod.rs:316-365 over build_full_trace mod.rs:434-524)
+ * produces, without the full trace in memory.  zkl_program_new executes the program once (same
+ * arguments as zkl_build_trace) and keeps the VM carry every 32 levels, the RAM event log with the
+ * sorted table's running sums, ROM lane 0, rom_acc and the Merkle root; *full_width_out /
+ * *n_rows_out receive the full trace's shape.  zkl_build_segment_trace then writes rows [r_start,
+ * r_end) in the segment's layout with its AIR public inputs and VM state hashes -- bit for bit
+ * what zkl_slice_segment(zkl_build_trace(..), .., r_start, r_end, ..) returns (same alignment
+ * rules; trace_out NULL: only *width_out).  Calls on one program may run concurrently.
+ * examples/fib-2pow16.zlisp (2^24 rows) is built this way segment by segment. */
+typedef struct zkl_program zkl_program;
+int zkl_program_new(const zkl_op* ops, uint32_t n_ops, const uint8_t program_id[32],
+                    const uint8_t program_commitment[32], const uint64_t* secret_args, uint32_t n_secret,
+                    const zkl_vm_arg* main_args, uint32_t n_main, const zkl_f128* rom0_in, zkl_program** out,
+                    uint32_t* full_width_out, uint32_t* n_rows_out);
+int zkl_build_segment_trace(const zkl_program* prog, uint32_t r_start, uint32_t r_end, zkl_f128* trace_out,
+                            zkl_air_public_inputs* pi_out, uint32_t* width_out, uint8_t state_in[32],
+                            uint8_t state_out[32]);
+void zkl_program_free(zkl_program* prog);
 
 /* ---- zl1 step proof (host-side, no device work) ----------------------------------
  * StepProof::to_bytes (proof/step.rs:79-151) of the step proof prove_segment builds around

@@ -127,6 +127,13 @@ int orc_build_trace(const zkl_op *ops, uint32_t n_ops, const uint8_t program_id[
                     const uint64_t *secret_args, uint32_t n_secret, const zkl_vm_arg *main_args, uint32_t n_main,
                     const zkl_f128 *rom0_in, zkl_f128 *trace_out, zkl_air_public_inputs *pi_out, uint32_t *width_out,
                     uint32_t *n_rows_out);
+/* per-segment builder, zkl_build_segment_trace's twin (program arguments as orc_build_trace,
+ * then the segment's rows; streams every level, no full trace) */
+int orc_build_segment_trace(const zkl_op *ops, uint32_t n_ops, const uint8_t program_id[32],
+                            const uint8_t commitment[32], const uint64_t *secret_args, uint32_t n_secret,
+                            const zkl_vm_arg *main_args, uint32_t n_main, const zkl_f128 *rom0_in, uint32_t r_start,
+                            uint32_t r_end, zkl_f128 *trace_out, zkl_air_public_inputs *pi_out, uint32_t *width_out,
+                            uint8_t state_in[32], uint8_t state_out[32]);
 int orc_prove_segment(const zkl_f128 *trace, uint32_t width, uint32_t n,
                       const zkl_air_public_inputs *pi, const zkl_proof_options *opts,
                       uint8_t **proof, size_t *len, int boundary_mode);

@@ -125,10 +125,10 @@ int orc_synth_vm_segment(uint64_t seed, uint32_t log_n, zkl_f128 *t, zkl_air_pub
 
 /* apply_level_absorb (vm/trace/poseidon.rs:9-87): lanes of one level hold the AIR-suite
  * permutation of [inputs (<= 10, zero padded), dom0, dom1]: map row = input state, round
- * row 1+j = state before round j, final and pad rows = output state */
-static void apply_level_absorb(zkl_f128 *t, size_t n, const zk_cols *c, const pos_suite *ps, size_t level,
-                               const fe *in, int nin) {
-  size_t b = level * 32;
+ * row 1+j = state before round j, final and pad rows = output state.  b = the level's map row
+ * in t; returns lane 0 of the output. */
+static fe apply_level_absorb(zkl_f128 *t, size_t n, const zk_cols *c, const pos_suite *ps, size_t b,
+                             const fe *in, int nin) {
   fe st[12];
   for (int i = 0; i < 12; i++) st[i] = 0;
   for (int i = 0; i < nin && i < 10; i++) st[i] = in[i];
@@ -148,6 +148,7 @@ static void apply_level_absorb(zkl_f128 *t, size_t n, const zk_cols *c, const po
   }
   for (size_t r = b + 28; r < b + 32; r++)
     for (int i = 0; i < 12; i++) set_fe(t, n, c->lanes_start + i, r, st[i]);
+  return st[0];
 }
 
 static void set_sponge_sel(zkl_f128 *t, size_t n, const zk_cols *c, size_t row, const int *regs, int k) {
@@ -244,292 +245,288 @@ int orc_synth_vm_segment_ex(uint64_t seed, uint32_t log_n, uint32_t flags, zkl_f
   return orc_synth_vm_segment_chain(seed, seed, log_n, flags, NULL, t, pi, width_out);
 }
 
-/* The trace of a program of `levels` ops (OP_PAD past its last op) and its AIR public inputs:
- * build_full_trace (mod.rs:434-524) with the initial registers regs0 (vm.rs:64-104), ROM lane 0
- * entering the first level = rom0, written in the segment layout of the features. */
-static int build_core(const synth_op *ops, size_t levels, const uint8_t pid[32], const uint8_t commit[32], int sponge,
-                      int ram, int merkle, fe rom0, const fe regs0[NR], const fe *slots, uint32_t n_slots, zkl_f128 *t,
-                      zkl_air_public_inputs *pi) {
-  size_t n = levels * 32;
-  zk_cols c;
-  cols_for_config(1, ram, sponge, merkle, 1, &c);
-  memset(t, 0, (size_t)c.width * n * sizeof(zkl_f128));
-  memset(pi, 0, sizeof *pi);
-  pos_suite ps;
-  pos_suite_derive(pid, POS_ROUNDS, &ps);
-
-  /* build_empty_trace + pc + dom tags (mod.rs:386-470) */
-  for (size_t l = 0; l < levels; l++) {
-    size_t b = l * 32;
-    set_fe(t, n, c.g_map, b, 1);
-    set_fe(t, n, c.g_final, b + 28, 1);
-    for (int j = 0; j < POS_ROUNDS; j++) set_fe(t, n, c.g_r_start + j, b + 1 + j, 1);
-    for (size_t r = b; r < b + 32; r++) set_fe(t, n, c.pc, r, (fe)l);
-    set_fe(t, n, c.lanes_start + 10, b, ps.dom[0]);
-    set_fe(t, n, c.lanes_start + 11, b, ps.dom[1]);
-  }
-  /* VmTraceBuilder (vm.rs:58-888) */
+/* The VM as it enters a level: registers, pending absorbs, the Merkle accumulator after the
+ * last Merkle level, host memory (addr -> value), the memory-event log (addr, clk, val,
+ * is_write), ROM lane 0 and the last ROM state. */
+typedef struct {
   fe regs[NR];
-  memcpy(regs, regs0, sizeof regs);
-  int pending[10], npending = 0;
-  /* RAM: host memory (addr -> value) and the event log (addr, clk, val, is_write) */
-  size_t n_ev = 0, n_mem = 0;
-  fe (*ev)[4] = (fe(*)[4])malloc((levels + 1) * sizeof *ev);
-  fe (*mem)[2] = (fe(*)[2])malloc((levels + 1) * sizeof *mem);
-  int last_merkle = -1;
-  for (size_t l = 0; l < levels; l++) {
-    fe next[NR];
-    memcpy(next, regs, sizeof next);
-    size_t b = l * 32, rm = b, rf = b + 28;
-    const synth_op *op = &ops[l];
-    if (op->kind == OP_PAD) continue; /* registers stay zero past the program (build_empty_trace) */
-    if (l == 0) set_fe(t, n, c.pi_prog, 0, be_from_le8(pid));
-    int onehot = -1;
-    switch (op->kind) {
-      case OP_CONST: onehot = 0; break;
-      case OP_MOV: onehot = 1; break;
-      case OP_ADD: onehot = 2; break;
-      case OP_SUB: onehot = 3; break;
-      case OP_MUL: onehot = 4; break;
-      case OP_NEG: onehot = 5; break;
-      case OP_EQ: onehot = 6; break;
-      case OP_SELECT: onehot = 7; break;
-      case OP_ASSERT: onehot = 9; break;
-      case OP_ASSERT_BIT: onehot = 10; break;
-      case OP_RANGE:
-      case OP_RANGE_LO:
-      case OP_RANGE_HI: onehot = 11; break;
-      case OP_DIVMOD: onehot = 12; break;
-      case OP_DIV128: onehot = 13; break;
-      case OP_MULWIDE: onehot = 14; break;
-      case OP_ABSORB:
-      case OP_SQUEEZE: onehot = 8; break;
-      case OP_CADDR: onehot = 0; break;
-      case OP_LOAD: onehot = 15; break;
-      case OP_STORE: onehot = 16; break;
-      default: break;
-    }
-    if (onehot >= 0) set_fe(t, n, c.rom_op_start + onehot, rm, 1);
-    for (int i = 0; i < NR; i++) set_fe(t, n, c.r_start + i, rm, regs[i]);
-    size_t rows[2] = {rm, rf};
-    if (op->kind == OP_ABSORB || op->kind == OP_SQUEEZE) {
-      /* SAbsorbN / SSqueeze (vm.rs:565-672): op_sponge and lane selectors at map and final */
-      int sel_regs[10], k = 0;
-      if (op->kind == OP_ABSORB) {
-        for (int i = 0; i < op->nabs; i++) {
-          if (npending == 10) { free(ev); free(mem); return -1; } /* push_absorb overflow (vm.rs:925-935) */
-          sel_regs[k++] = op->abs_regs[i];
-          pending[npending++] = op->abs_regs[i];
-        }
-      } else {
-        for (int i = 0; i < npending; i++) sel_regs[k++] = pending[i];
-      }
-      for (int q = 0; q < 2; q++) {
-        set_fe(t, n, c.op[8], rows[q], 1);
-        set_sponge_sel(t, n, &c, rows[q], sel_regs, k);
-      }
-      if (op->kind == OP_SQUEEZE) {
-        set_sel(t, n, rf, c.sel_dst0, op->dst);
-        fe in[10];
-        for (int i = 0; i < k; i++) in[i] = regs[sel_regs[i]];
-        apply_level_absorb(t, n, &c, &ps, l, in, k);
-        next[op->dst] = get_fe(t, n, c.lanes_start, rf);
-        npending = 0;
-        for (size_t r = b; r < b + 32; r++) set_fe(t, n, c.pose_active, r, 1);
-      }
-    }
-    if (op->kind == OP_MFIRST || op->kind == OP_MSTEP || op->kind == OP_MLAST) {
-      /* MerkleStepFirst / MerkleStep / MerkleStepLast (vm.rs:675-800) */
-      for (size_t r = b; r < b + 32; r++) set_fe(t, n, c.merkle_g, r, 1);
-      fe acc;
-      if (op->kind == OP_MFIRST) {
-        acc = regs[op->dst];
-        set_fe(t, n, c.merkle_first, rm, 1);
-        set_fe(t, n, c.merkle_leaf, rm, acc);
-      } else {
-        acc = last_merkle >= 0 ? get_fe(t, n, c.merkle_acc, (size_t)last_merkle * 32 + 28) : 0;
-      }
-      for (size_t r = rm; r < rf; r++) set_fe(t, n, c.merkle_acc, r, acc);
-      fe d = regs[op->a], sib = regs[op->b];
-      set_fe(t, n, c.merkle_dir, rm, d);
-      set_fe(t, n, c.merkle_sib, rm, sib);
-      fe in[2] = {fe_add(fe_mul(fe_sub(1, d), acc), fe_mul(d, sib)), fe_add(fe_mul(fe_sub(1, d), sib), fe_mul(d, acc))};
-      apply_level_absorb(t, n, &c, &ps, l, in, 2);
-      if (op->kind == OP_MLAST) set_fe(t, n, c.merkle_last, rf, 1);
-      fe out = get_fe(t, n, c.lanes_start, rf);
-      for (size_t r = rf; r < b + 32; r++) set_fe(t, n, c.merkle_acc, r, out);
-      for (size_t r = b; r < b + 32; r++) set_fe(t, n, c.pose_active, r, 1);
-      last_merkle = (int)l;
-    }
-    if (op->kind == OP_LOAD || op->kind == OP_STORE) {
-      /* Load / Store (vm.rs:803-842): clk = level, loads read 0 from unwritten addresses */
-      fe addr = regs[op->a], val = 0;
-      size_t k = 0;
-      while (k < n_mem && mem[k][0] != addr) k++;
-      for (int q = 0; q < 2; q++) {
-        set_fe(t, n, c.op[onehot], rows[q], 1);
-        set_sel(t, n, rows[q], c.sel_a, op->a);
-        if (op->kind == OP_LOAD) set_sel(t, n, rows[q], c.sel_dst0, op->dst);
-        else set_sel(t, n, rows[q], c.sel_b, op->b);
-      }
-      if (op->kind == OP_LOAD) {
-        val = k < n_mem ? mem[k][1] : 0;
-        set_fe(t, n, c.imm, rm, val);
-        set_fe(t, n, c.imm, rf, val);
-        next[op->dst] = val;
-      } else {
-        val = regs[op->b];
-        if (k == n_mem) { mem[k][0] = addr; n_mem++; }
-        mem[k][1] = val;
-      }
-      ev[n_ev][0] = addr; ev[n_ev][1] = (fe)l; ev[n_ev][2] = val; ev[n_ev][3] = op->kind == OP_STORE;
-      n_ev++;
-    }
-    /* ALU ops (vm.rs:199-564): op bit and selectors on map and final rows, imm / eq_inv /
-     * range-gadget witnesses on both rows */
-    const int k_ = op->kind;
-    const fe M64 = (((fe)1) << 64) - 1;
-    fe ra = regs[op->a], rb = regs[op->b], rc = regs[op->c];
-    fe imm = 0, inv = 0, bitv[32];
-    int gadget = 0;
-    switch (k_) {
-      case OP_CONST:
-      case OP_CADDR: imm = (fe)op->imm; next[op->dst] = imm; break;
-      case OP_MOV: next[op->dst] = ra; break;
-      case OP_ADD: next[op->dst] = fe_add(ra, rb); break;
-      case OP_SUB: next[op->dst] = fe_sub(ra, rb); break;
-      case OP_MUL: next[op->dst] = fe_mul(ra, rb); break;
-      case OP_NEG: next[op->dst] = fe_neg(ra); break;
-      case OP_EQ: {
-        fe d = fe_sub(ra, rb);
-        inv = d ? fe_inv(d) : 0;
-        next[op->dst] = d ? 0 : 1;
-        break;
-      }
-      case OP_SELECT: next[op->dst] = fe_add(fe_mul(rc, ra), fe_mul(fe_sub(1, rc), rb)); break;
-      case OP_ASSERT:
-      case OP_ASSERT_BIT: next[op->dst] = 1; break;
-      case OP_RANGE: { /* 32-bit form: imm 1, eq_inv 0, the low min(bits, 32) bits of r */
-        int kb = op->bits < 32 ? op->bits : 32;
-        for (int i = 0; i < 32; i++) bitv[i] = i < kb ? (rc >> i) & 1 : 0;
-        imm = 1; gadget = 1;
-        next[op->dst] = 1;
-        break;
-      }
-      case OP_RANGE_LO: /* 64-bit stage 0: imm 0, eq_inv 1, low 32 bits; dst <- r mod 2^32 */
-        for (int i = 0; i < 32; i++) bitv[i] = (rc >> i) & 1;
-        inv = 1; gadget = 1;
-        next[op->dst] = rc & 0xFFFFFFFFu;
-        break;
-      case OP_RANGE_HI: /* stage 1: imm 1, eq_inv 1, bits 32..63 */
-        for (int i = 0; i < 32; i++) bitv[i] = (rc >> (32 + i)) & 1;
-        imm = 1; inv = 1; gadget = 1;
-        next[op->dst] = 1;
-        break;
-      case OP_DIVMOD: { /* canonical values as u128; results mod 2^64; eq_inv = (b mod 2^64)^-1 */
-        fe q = rb ? ra / rb : 0, r = rb ? ra % rb : ra;
-        next[op->dst] = q & M64;
-        next[op->dst2] = r & M64;
-        inv = rb ? fe_inv(rb & M64) : 0;
-        break;
-      }
-      case OP_MULWIDE: {
-        fe prod = (ra & M64) * (rb & M64);
-        next[op->dst] = prod & M64;
-        next[op->dst2] = prod >> 64;
-        break;
-      }
-      case OP_DIV128: { /* ((a_hi << 64) | a_lo mod 2^64) / b; imm = a_lo */
-        fe num = (ra << 64) | (rc & M64);
-        fe q = rb ? num / rb : 0, r = rb ? num % rb : num;
-        imm = rc;
-        next[op->dst] = q & M64;
-        next[op->dst2] = r & M64;
-        inv = rb ? fe_inv(rb & M64) : 0;
-        break;
-      }
-      default: break;
-    }
-    if (onehot >= 0 && onehot != 8 && onehot < 15) {
-      int uses_a = k_ != OP_CONST && k_ != OP_CADDR && k_ != OP_ASSERT && k_ != OP_ASSERT_BIT && k_ != OP_RANGE &&
-                   k_ != OP_RANGE_LO && k_ != OP_RANGE_HI;
-      int uses_b = k_ == OP_ADD || k_ == OP_SUB || k_ == OP_MUL || k_ == OP_EQ || k_ == OP_SELECT || k_ == OP_DIVMOD ||
-                   k_ == OP_DIV128 || k_ == OP_MULWIDE;
-      int uses_c = k_ == OP_SELECT || k_ == OP_ASSERT || k_ == OP_ASSERT_BIT || k_ == OP_RANGE || k_ == OP_RANGE_LO ||
-                   k_ == OP_RANGE_HI;
-      int uses_d1 = k_ == OP_DIVMOD || k_ == OP_DIV128 || k_ == OP_MULWIDE;
-      for (int q = 0; q < 2; q++) {
-        size_t row = rows[q];
-        set_fe(t, n, c.op[onehot], row, 1);
-        set_sel(t, n, row, c.sel_dst0, op->dst);
-        if (uses_d1) set_sel(t, n, row, c.sel_dst1, op->dst2);
-        if (uses_a) set_sel(t, n, row, c.sel_a, op->a);
-        if (uses_b) set_sel(t, n, row, c.sel_b, op->b);
-        if (uses_c) set_sel(t, n, row, c.sel_c, op->c);
-        set_fe(t, n, c.imm, row, imm);
-        set_fe(t, n, c.eq_inv, row, inv);
-        for (int i = 0; gadget && i < 32; i++) set_fe(t, n, c.gadget_b + i, row, bitv[i]);
-      }
-    }
-    for (size_t r = rm + 1; r <= rf; r++)
-      for (int i = 0; i < NR; i++) set_fe(t, n, c.r_start + i, r, regs[i]);
-    for (size_t r = rf + 1; r < b + 32; r++)
-      for (int i = 0; i < NR; i++) set_fe(t, n, c.r_start + i, r, next[i]);
-    memcpy(regs, next, sizeof regs);
-  }
-  if (ram) ram_fill(t, n, &c, pid, ev, n_ev);
-  free(ev);
-  free(mem);
-  /* RomTraceBuilder (rom.rs:37-106) */
-  fe rc3[POS_ROUNDS][3], mds3[3][3], w0[59], w1[59];
-  rom_constants(pid, rc3, mds3);
-  {
-    fe a = fe_exp(3, 17), cur = fe_mul(a, 3);
-    for (int i = 0; i < 59; i++) { w0[i] = cur; cur = fe_mul(cur, 3); }
-    a = fe_exp(3, 1037); cur = fe_mul(a, 3);
-    for (int i = 0; i < 59; i++) { w1[i] = cur; cur = fe_mul(cur, 3); }
-  }
-  fe s0_prev = rom0;
-  fe last_state[3] = {0, 0, 0};
-  for (size_t l = 0; l < levels; l++) {
-    size_t b = l * 32, rm = b, rf = b + 28;
-    fe s1 = rom_encode_row(&c, t, n, rm, w0), s2 = rom_encode_row(&c, t, n, rm, w1);
-    set_fe(t, n, c.rom_s, rm, s0_prev);
-    set_fe(t, n, c.rom_s + 1, rm, s1);
-    set_fe(t, n, c.rom_s + 2, rm, s2);
-    fe s[3] = {s0_prev, s1, s2};
-    for (int j = 0; j < POS_ROUNDS; j++) {
-      size_t r = b + 1 + j;
-      for (int i = 0; i < 3; i++) set_fe(t, n, c.rom_s + i, r, s[i]);
-      fe s3[3] = {fe_cube(s[0]), fe_cube(s[1]), fe_cube(s[2])};
-      fe y[3];
-      for (int i = 0; i < 3; i++)
-        y[i] = fe_add(fe_add(fe_add(fe_mul(mds3[i][0], s3[0]), fe_mul(mds3[i][1], s3[1])),
-                             fe_mul(mds3[i][2], s3[2])), rc3[j][i]);
-      for (int i = 0; i < 3; i++) set_fe(t, n, c.rom_s + i, r + 1, y[i]);
-      memcpy(s, y, sizeof s);
-    }
-    for (size_t r = rf + 1; r < b + 32; r++)
-      for (int i = 0; i < 3; i++) set_fe(t, n, c.rom_s + i, r, s[i]);
-    s0_prev = s[0];
-    memcpy(last_state, s, sizeof s);
-  }
+  int pending[10], npending;
+  fe merkle_out;
+  long mlast;     /* last MerkleStepLast level (-1: none) */
+  fe merkle_root; /* the accumulator after it */
+  fe (*ev)[4];
+  size_t n_ev;
+  fe (*mem)[2];
+  size_t n_mem;
+  fe rom_s0, rom_state[3];
+} orc_vm;
 
-  /* AIR public inputs (prove.rs:292-423 with segment = whole trace) */
-  memcpy(pi->program_id, pid, 32);
-  memcpy(pi->program_commitment, commit, 32);
-  pi->feature_mask = FM_VM | (sponge ? FM_SPONGE | FM_POSEIDON : 0) | (ram ? FM_RAM : 0) |
-                     (merkle ? FM_MERKLE | FM_POSEIDON : 0);
-  long mlast = -1;
-  for (size_t l = 0; l < levels; l++) if (ops[l].kind == OP_MLAST) mlast = (long)l;
-  if (merkle && mlast >= 0) { /* root = acc after the last MerkleStepLast level, 16 LE bytes (utils.rs:346-355) */
-    fe root = get_fe(t, n, c.merkle_acc, (size_t)mlast * 32 + 28);
-    for (int i = 0; i < 16; i++) pi->merkle_root[i] = (uint8_t)(root >> (8 * i));
+typedef struct { fe rc3[POS_ROUNDS][3], mds3[3][3], w0[59], w1[59]; } rom_k;
+
+static int op_onehot(int kind) {
+  switch (kind) {
+    case OP_CONST: case OP_CADDR: return 0;
+    case OP_MOV: return 1;
+    case OP_ADD: return 2;
+    case OP_SUB: return 3;
+    case OP_MUL: return 4;
+    case OP_NEG: return 5;
+    case OP_EQ: return 6;
+    case OP_SELECT: return 7;
+    case OP_ABSORB: case OP_SQUEEZE: return 8;
+    case OP_ASSERT: return 9;
+    case OP_ASSERT_BIT: return 10;
+    case OP_RANGE: case OP_RANGE_LO: case OP_RANGE_HI: return 11;
+    case OP_DIVMOD: return 12;
+    case OP_DIV128: return 13;
+    case OP_MULWIDE: return 14;
+    case OP_LOAD: return 15;
+    case OP_STORE: return 16;
+    default: return -1;
   }
-  pi->segment_feature_mask = pi->feature_mask;
-  pi->n_main_slots = n_slots;
-  for (uint32_t i = 0; i < n_slots; i++) { pi->main_slots[i].lo = (uint64_t)slots[i]; pi->main_slots[i].hi = (uint64_t)(slots[i] >> 64); }
-  /* vm_output_from_trace_with_layout (utils.rs:262-289) */
+}
+
+/* One level of build_full_trace: build_empty_trace's gates, pc and dom tags (mod.rs:386-470)
+ * and VmTraceBuilder::fill_table for its op (vm.rs:58-888), written to rows [b, b + 32) of t
+ * (n rows) for level l. */
+static int level_fill(zkl_f128 *t, size_t n, size_t b, size_t l, const synth_op *op, const zk_cols *cp,
+                      const pos_suite *ps, const uint8_t pid[32], orc_vm *vm) {
+  const zk_cols c = *cp;
+  set_fe(t, n, c.g_map, b, 1);
+  set_fe(t, n, c.g_final, b + 28, 1);
+  for (int j = 0; j < POS_ROUNDS; j++) set_fe(t, n, c.g_r_start + j, b + 1 + j, 1);
+  for (size_t r = b; r < b + 32; r++) set_fe(t, n, c.pc, r, (fe)l);
+  set_fe(t, n, c.lanes_start + 10, b, ps->dom[0]);
+  set_fe(t, n, c.lanes_start + 11, b, ps->dom[1]);
+  if (op->kind == OP_PAD) return 0; /* registers stay zero past the program (build_empty_trace) */
+  fe *regs = vm->regs;
+  fe next[NR];
+  memcpy(next, regs, sizeof next);
+  size_t rm = b, rf = b + 28;
+  if (l == 0) set_fe(t, n, c.pi_prog, 0, be_from_le8(pid));
+  int onehot = op_onehot(op->kind);
+  if (onehot >= 0) set_fe(t, n, c.rom_op_start + onehot, rm, 1);
+  for (int i = 0; i < NR; i++) set_fe(t, n, c.r_start + i, rm, regs[i]);
+  size_t rows[2] = {rm, rf};
+  if (op->kind == OP_ABSORB || op->kind == OP_SQUEEZE) {
+    /* SAbsorbN / SSqueeze (vm.rs:565-672): op_sponge and lane selectors at map and final */
+    int sel_regs[10], k = 0;
+    if (op->kind == OP_ABSORB) {
+      for (int i = 0; i < op->nabs; i++) {
+        if (vm->npending == 10) return -1; /* push_absorb overflow (vm.rs:925-935) */
+        sel_regs[k++] = op->abs_regs[i];
+        vm->pending[vm->npending++] = op->abs_regs[i];
+      }
+    } else {
+      for (int i = 0; i < vm->npending; i++) sel_regs[k++] = vm->pending[i];
+    }
+    for (int q = 0; q < 2; q++) {
+      set_fe(t, n, c.op[8], rows[q], 1);
+      set_sponge_sel(t, n, &c, rows[q], sel_regs, k);
+    }
+    if (op->kind == OP_SQUEEZE) {
+      set_sel(t, n, rf, c.sel_dst0, op->dst);
+      fe in[10];
+      for (int i = 0; i < k; i++) in[i] = regs[sel_regs[i]];
+      next[op->dst] = apply_level_absorb(t, n, &c, ps, b, in, k);
+      vm->npending = 0;
+      for (size_t r = b; r < b + 32; r++) set_fe(t, n, c.pose_active, r, 1);
+    }
+  }
+  if (op->kind == OP_MFIRST || op->kind == OP_MSTEP || op->kind == OP_MLAST) {
+    /* MerkleStepFirst / MerkleStep / MerkleStepLast (vm.rs:675-800) */
+    for (size_t r = b; r < b + 32; r++) set_fe(t, n, c.merkle_g, r, 1);
+    fe acc;
+    if (op->kind == OP_MFIRST) {
+      acc = regs[op->dst];
+      set_fe(t, n, c.merkle_first, rm, 1);
+      set_fe(t, n, c.merkle_leaf, rm, acc);
+    } else {
+      acc = vm->merkle_out;
+    }
+    for (size_t r = rm; r < rf; r++) set_fe(t, n, c.merkle_acc, r, acc);
+    fe d = regs[op->a], sib = regs[op->b];
+    set_fe(t, n, c.merkle_dir, rm, d);
+    set_fe(t, n, c.merkle_sib, rm, sib);
+    fe in[2] = {fe_add(fe_mul(fe_sub(1, d), acc), fe_mul(d, sib)), fe_add(fe_mul(fe_sub(1, d), sib), fe_mul(d, acc))};
+    fe out = apply_level_absorb(t, n, &c, ps, b, in, 2);
+    if (op->kind == OP_MLAST) {
+      set_fe(t, n, c.merkle_last, rf, 1);
+      vm->mlast = (long)l;
+      vm->merkle_root = out;
+    }
+    for (size_t r = rf; r < b + 32; r++) set_fe(t, n, c.merkle_acc, r, out);
+    for (size_t r = b; r < b + 32; r++) set_fe(t, n, c.pose_active, r, 1);
+    vm->merkle_out = out;
+  }
+  if (op->kind == OP_LOAD || op->kind == OP_STORE) {
+    /* Load / Store (vm.rs:803-842): clk = level, loads read 0 from unwritten addresses */
+    fe addr = regs[op->a], val = 0;
+    size_t k = 0;
+    while (k < vm->n_mem && vm->mem[k][0] != addr) k++;
+    for (int q = 0; q < 2; q++) {
+      set_fe(t, n, c.op[onehot], rows[q], 1);
+      set_sel(t, n, rows[q], c.sel_a, op->a);
+      if (op->kind == OP_LOAD) set_sel(t, n, rows[q], c.sel_dst0, op->dst);
+      else set_sel(t, n, rows[q], c.sel_b, op->b);
+    }
+    if (op->kind == OP_LOAD) {
+      val = k < vm->n_mem ? vm->mem[k][1] : 0;
+      set_fe(t, n, c.imm, rm, val);
+      set_fe(t, n, c.imm, rf, val);
+      next[op->dst] = val;
+    } else {
+      val = regs[op->b];
+      if (k == vm->n_mem) { vm->mem[k][0] = addr; vm->n_mem++; }
+      vm->mem[k][1] = val;
+    }
+    fe *e = vm->ev[vm->n_ev++];
+    e[0] = addr; e[1] = (fe)l; e[2] = val; e[3] = op->kind == OP_STORE;
+  }
+  /* ALU ops (vm.rs:199-564): op bit and selectors on map and final rows, imm / eq_inv /
+   * range-gadget witnesses on both rows */
+  const int k_ = op->kind;
+  const fe M64 = (((fe)1) << 64) - 1;
+  fe ra = regs[op->a], rb = regs[op->b], rc = regs[op->c];
+  fe imm = 0, inv = 0, bitv[32];
+  int gadget = 0;
+  switch (k_) {
+    case OP_CONST:
+    case OP_CADDR: imm = (fe)op->imm; next[op->dst] = imm; break;
+    case OP_MOV: next[op->dst] = ra; break;
+    case OP_ADD: next[op->dst] = fe_add(ra, rb); break;
+    case OP_SUB: next[op->dst] = fe_sub(ra, rb); break;
+    case OP_MUL: next[op->dst] = fe_mul(ra, rb); break;
+    case OP_NEG: next[op->dst] = fe_neg(ra); break;
+    case OP_EQ: {
+      fe d = fe_sub(ra, rb);
+      inv = d ? fe_inv(d) : 0;
+      next[op->dst] = d ? 0 : 1;
+      break;
+    }
+    case OP_SELECT: next[op->dst] = fe_add(fe_mul(rc, ra), fe_mul(fe_sub(1, rc), rb)); break;
+    case OP_ASSERT:
+    case OP_ASSERT_BIT: next[op->dst] = 1; break;
+    case OP_RANGE: { /* 32-bit form: imm 1, eq_inv 0, the low min(bits, 32) bits of r */
+      int kb = op->bits < 32 ? op->bits : 32;
+      for (int i = 0; i < 32; i++) bitv[i] = i < kb ? (rc >> i) & 1 : 0;
+      imm = 1; gadget = 1;
+      next[op->dst] = 1;
+      break;
+    }
+    case OP_RANGE_LO: /* 64-bit stage 0: imm 0, eq_inv 1, low 32 bits; dst <- r mod 2^32 */
+      for (int i = 0; i < 32; i++) bitv[i] = (rc >> i) & 1;
+      inv = 1; gadget = 1;
+      next[op->dst] = rc & 0xFFFFFFFFu;
+      break;
+    case OP_RANGE_HI: /* stage 1: imm 1, eq_inv 1, bits 32..63 */
+      for (int i = 0; i < 32; i++) bitv[i] = (rc >> (32 + i)) & 1;
+      imm = 1; inv = 1; gadget = 1;
+      next[op->dst] = 1;
+      break;
+    case OP_DIVMOD: { /* canonical values as u128; results mod 2^64; eq_inv = (b mod 2^64)^-1 */
+      fe q = rb ? ra / rb : 0, r = rb ? ra % rb : ra;
+      next[op->dst] = q & M64;
+      next[op->dst2] = r & M64;
+      inv = rb ? fe_inv(rb & M64) : 0;
+      break;
+    }
+    case OP_MULWIDE: {
+      fe prod = (ra & M64) * (rb & M64);
+      next[op->dst] = prod & M64;
+      next[op->dst2] = prod >> 64;
+      break;
+    }
+    case OP_DIV128: { /* ((a_hi << 64) | a_lo mod 2^64) / b; imm = a_lo */
+      fe num = (ra << 64) | (rc & M64);
+      fe q = rb ? num / rb : 0, r = rb ? num % rb : num;
+      imm = rc;
+      next[op->dst] = q & M64;
+      next[op->dst2] = r & M64;
+      inv = rb ? fe_inv(rb & M64) : 0;
+      break;
+    }
+    default: break;
+  }
+  if (onehot >= 0 && onehot != 8 && onehot < 15) {
+    int uses_a = k_ != OP_CONST && k_ != OP_CADDR && k_ != OP_ASSERT && k_ != OP_ASSERT_BIT && k_ != OP_RANGE &&
+                 k_ != OP_RANGE_LO && k_ != OP_RANGE_HI;
+    int uses_b = k_ == OP_ADD || k_ == OP_SUB || k_ == OP_MUL || k_ == OP_EQ || k_ == OP_SELECT || k_ == OP_DIVMOD ||
+                 k_ == OP_DIV128 || k_ == OP_MULWIDE;
+    int uses_c = k_ == OP_SELECT || k_ == OP_ASSERT || k_ == OP_ASSERT_BIT || k_ == OP_RANGE || k_ == OP_RANGE_LO ||
+                 k_ == OP_RANGE_HI;
+    int uses_d1 = k_ == OP_DIVMOD || k_ == OP_DIV128 || k_ == OP_MULWIDE;
+    for (int q = 0; q < 2; q++) {
+      size_t row = rows[q];
+      set_fe(t, n, c.op[onehot], row, 1);
+      set_sel(t, n, row, c.sel_dst0, op->dst);
+      if (uses_d1) set_sel(t, n, row, c.sel_dst1, op->dst2);
+      if (uses_a) set_sel(t, n, row, c.sel_a, op->a);
+      if (uses_b) set_sel(t, n, row, c.sel_b, op->b);
+      if (uses_c) set_sel(t, n, row, c.sel_c, op->c);
+      set_fe(t, n, c.imm, row, imm);
+      set_fe(t, n, c.eq_inv, row, inv);
+      for (int i = 0; gadget && i < 32; i++) set_fe(t, n, c.gadget_b + i, row, bitv[i]);
+    }
+  }
+  for (size_t r = rm + 1; r <= rf; r++)
+    for (int i = 0; i < NR; i++) set_fe(t, n, c.r_start + i, r, regs[i]);
+  for (size_t r = rf + 1; r < b + 32; r++)
+    for (int i = 0; i < NR; i++) set_fe(t, n, c.r_start + i, r, next[i]);
+  memcpy(regs, next, sizeof next);
+  return 0;
+}
+
+static void rom_k_init(const uint8_t pid[32], rom_k *k) {
+  rom_constants(pid, k->rc3, k->mds3);
+  fe a = fe_exp(3, 17), cur = fe_mul(a, 3);
+  for (int i = 0; i < 59; i++) { k->w0[i] = cur; cur = fe_mul(cur, 3); }
+  a = fe_exp(3, 1037); cur = fe_mul(a, 3);
+  for (int i = 0; i < 59; i++) { k->w1[i] = cur; cur = fe_mul(cur, 3); }
+}
+
+/* RomTraceBuilder (rom.rs:37-106) for the level whose map row is b: lane 0 carried in, lanes
+ * 1, 2 the two encodings of the map row, 27 rounds of the t=3 permutation */
+static void level_rom(zkl_f128 *t, size_t n, size_t b, const zk_cols *c, const rom_k *k, orc_vm *vm) {
+  size_t rf = b + 28;
+  fe s[3] = {vm->rom_s0, rom_encode_row(c, t, n, b, k->w0), rom_encode_row(c, t, n, b, k->w1)};
+  for (int i = 0; i < 3; i++) set_fe(t, n, c->rom_s + i, b, s[i]);
+  for (int j = 0; j < POS_ROUNDS; j++) {
+    size_t r = b + 1 + j;
+    for (int i = 0; i < 3; i++) set_fe(t, n, c->rom_s + i, r, s[i]);
+    fe s3[3] = {fe_cube(s[0]), fe_cube(s[1]), fe_cube(s[2])};
+    fe y[3];
+    for (int i = 0; i < 3; i++)
+      y[i] = fe_add(fe_add(fe_add(fe_mul(k->mds3[i][0], s3[0]), fe_mul(k->mds3[i][1], s3[1])),
+                           fe_mul(k->mds3[i][2], s3[2])), k->rc3[j][i]);
+    for (int i = 0; i < 3; i++) set_fe(t, n, c->rom_s + i, r + 1, y[i]);
+    memcpy(s, y, sizeof s);
+  }
+  for (size_t r = rf + 1; r < b + 32; r++)
+    for (int i = 0; i < 3; i++) set_fe(t, n, c->rom_s + i, r, s[i]);
+  vm->rom_s0 = s[0];
+  memcpy(vm->rom_state, s, sizeof s);
+}
+
+static int vm_init(orc_vm *vm, size_t levels, const fe regs0[NR], fe rom0) {
+  memset(vm, 0, sizeof *vm);
+  memcpy(vm->regs, regs0, sizeof vm->regs);
+  vm->mlast = -1;
+  vm->rom_s0 = rom0;
+  vm->ev = (fe(*)[4])malloc((levels + 1) * sizeof *vm->ev);
+  vm->mem = (fe(*)[2])malloc((levels + 1) * sizeof *vm->mem);
+  return vm->ev && vm->mem ? 0 : -1;
+}
+static void vm_free(orc_vm *vm) {
+  free(vm->ev);
+  free(vm->mem);
+}
+
+/* vm_output_from_trace_with_layout (utils.rs:262-289) and compute_vm_usage_mask_for_trace
+ * (prove.rs:1289-1392) of a (segment) trace t of n rows in layout c */
+static void trace_pi(const zkl_f128 *t, size_t n, const zk_cols *cp, int ram, zkl_air_public_inputs *pi) {
+  const zk_cols c = *cp;
+  size_t levels = n / 32;
   pi->vm_out_reg = 0; pi->vm_out_row = 29;
   for (size_t l = levels; l-- > 0;) {
     size_t rf = l * 32 + 28;
@@ -537,17 +534,6 @@ static int build_core(const synth_op *ops, size_t levels, const uint8_t pid[32],
     for (int i = 0; i < NR; i++) if (get_fe(t, n, c.sel_dst0 + i, rf) == 1) { found = i; break; }
     if (found >= 0) { pi->vm_out_reg = (uint32_t)found; pi->vm_out_row = (uint32_t)(rf + 1); break; }
   }
-  for (int i = 0; i < 3; i++) {
-    fe v = last_state[i];
-    pi->rom_acc[i].lo = (uint64_t)v; pi->rom_acc[i].hi = (uint64_t)(v >> 64);
-    fe in = get_fe(t, n, c.rom_s + i, 0);
-    pi->rom_s_in[i].lo = (uint64_t)in; pi->rom_s_in[i].hi = (uint64_t)(in >> 64);
-    fe out = get_fe(t, n, c.rom_s + i, (levels - 1) * 32 + 28);
-    pi->rom_s_out[i].lo = (uint64_t)out; pi->rom_s_out[i].hi = (uint64_t)(out >> 64);
-  }
-  fe pc0 = get_fe(t, n, c.pc, 0);
-  pi->pc_init.lo = (uint64_t)pc0; pi->pc_init.hi = (uint64_t)(pc0 >> 64);
-  /* compute_vm_usage_mask_for_trace (prove.rs:1289-1392): ALU-only program -> 0 */
   uint32_t mask = 0;
   for (size_t r = 0; r < n; r++) {
     int at_final = (r % 32) == 28;
@@ -570,6 +556,57 @@ static int build_core(const synth_op *ops, size_t levels, const uint8_t pid[32],
       }
   pi->vm_usage_mask = mask;
   pi->ram_delta_clk_bits = ram_bits;
+}
+
+static void put_fe(zkl_f128 *d, fe v) { d->lo = (uint64_t)v; d->hi = (uint64_t)(v >> 64); }
+
+/* the program-level public inputs (prove.rs:292-423): ids, commitment, feature mask, main-arg
+ * slots, merkle_root (the accumulator after the last MerkleStepLast, 16 LE bytes,
+ * utils.rs:346-355), rom_acc = the ROM state after the last level */
+static void program_pi(const orc_vm *vm, const uint8_t pid[32], const uint8_t commit[32], int sponge, int ram,
+                       int merkle, const fe *slots, uint32_t n_slots, zkl_air_public_inputs *pi) {
+  memset(pi, 0, sizeof *pi);
+  memcpy(pi->program_id, pid, 32);
+  memcpy(pi->program_commitment, commit, 32);
+  pi->feature_mask = FM_VM | (sponge ? FM_SPONGE | FM_POSEIDON : 0) | (ram ? FM_RAM : 0) |
+                     (merkle ? FM_MERKLE | FM_POSEIDON : 0);
+  pi->segment_feature_mask = pi->feature_mask;
+  if (merkle && vm->mlast >= 0)
+    for (int i = 0; i < 16; i++) pi->merkle_root[i] = (uint8_t)(vm->merkle_root >> (8 * i));
+  pi->n_main_slots = n_slots;
+  for (uint32_t i = 0; i < n_slots; i++) put_fe(&pi->main_slots[i], slots[i]);
+  for (int i = 0; i < 3; i++) put_fe(&pi->rom_acc[i], vm->rom_state[i]);
+}
+
+/* The trace of a program of `levels` ops (OP_PAD past its last op) and its AIR public inputs:
+ * build_full_trace (mod.rs:434-524) with the initial registers regs0 (vm.rs:64-104), ROM lane 0
+ * entering the first level = rom0, written in the segment layout of the features. */
+static int build_core(const synth_op *ops, size_t levels, const uint8_t pid[32], const uint8_t commit[32], int sponge,
+                      int ram, int merkle, fe rom0, const fe regs0[NR], const fe *slots, uint32_t n_slots, zkl_f128 *t,
+                      zkl_air_public_inputs *pi) {
+  size_t n = levels * 32;
+  zk_cols c;
+  cols_for_config(1, ram, sponge, merkle, 1, &c);
+  memset(t, 0, (size_t)c.width * n * sizeof(zkl_f128));
+  pos_suite ps;
+  pos_suite_derive(pid, POS_ROUNDS, &ps);
+  rom_k rk;
+  rom_k_init(pid, &rk);
+  orc_vm vm;
+  if (vm_init(&vm, levels, regs0, rom0)) { vm_free(&vm); return -1; }
+  for (size_t l = 0; l < levels; l++) {
+    if (level_fill(t, n, l * 32, l, &ops[l], &c, &ps, pid, &vm)) { vm_free(&vm); return -1; }
+    level_rom(t, n, l * 32, &c, &rk, &vm);
+  }
+  if (ram) ram_fill(t, n, &c, pid, vm.ev, vm.n_ev);
+  program_pi(&vm, pid, commit, sponge, ram, merkle, slots, n_slots, pi);
+  vm_free(&vm);
+  for (int i = 0; i < 3; i++) {
+    put_fe(&pi->rom_s_in[i], get_fe(t, n, c.rom_s + i, 0));
+    put_fe(&pi->rom_s_out[i], get_fe(t, n, c.rom_s + i, (levels - 1) * 32 + 28));
+  }
+  put_fe(&pi->pc_init, get_fe(t, n, c.pc, 0));
+  trace_pi(t, n, &c, ram, pi);
   return 0;
 }
 
@@ -599,20 +636,29 @@ int orc_synth_vm_segment_chain(uint64_t program_seed, uint64_t seed, uint32_t lo
   return rc;
 }
 
-/* The op-list trace builder (zkl_build_trace's twin): builder::Op list (builder.rs:25-158)
- * -> build_full_trace (mod.rs:434-524) over next_pow2(n_ops) levels. */
-int orc_build_trace(const zkl_op *zops, uint32_t n_ops, const uint8_t pid[32], const uint8_t commit[32],
-                    const uint64_t *secret, uint32_t n_secret, const zkl_vm_arg *margs, uint32_t n_main,
-                    const zkl_f128 *rom0_in, zkl_f128 *t, zkl_air_public_inputs *pi, uint32_t *width_out,
-                    uint32_t *n_rows_out) {
+/* builder::Op list (builder.rs:25-158) -> one synth_op per level over next_pow2(n_ops) levels
+ * (OP_PAD past the last op), the features, and the initial registers: secret u64 args from r0,
+ * main args as base-field slots (encode_vmarg_to_elements, utils.rs:79-97) in the tail registers
+ * (vm.rs:64-104).  Returns the op array (free) or NULL. */
+typedef struct {
+  synth_op *ops;
+  size_t levels, n_ops;
+  int sponge, ram, merkle;
+  fe regs0[NR], slots[8];
+  uint32_t n_slots;
+} orc_prog;
+
+static int parse_program(const zkl_op *zops, uint32_t n_ops, const uint64_t *secret, uint32_t n_secret,
+                         const zkl_vm_arg *margs, uint32_t n_main, orc_prog *P) {
   static const int kinds[] = {OP_CONST, OP_MOV, OP_ADD, OP_SUB, OP_MUL, OP_NEG, OP_EQ, OP_SELECT, OP_ASSERT,
                               OP_ASSERT_BIT, OP_RANGE, OP_RANGE_LO, OP_RANGE_HI, OP_DIVMOD, OP_DIV128, OP_MULWIDE,
                               OP_LOAD, OP_STORE, OP_ABSORB, OP_SQUEEZE, OP_MFIRST, OP_MSTEP, OP_MLAST, OP_END};
+  memset(P, 0, sizeof *P);
   if (!zops || !n_ops || n_main > ZKL_MAX_MAIN_SLOTS) return -1;
   size_t levels = 1;
   while (levels < n_ops) levels <<= 1;
   synth_op *ops = (synth_op *)calloc(levels, sizeof(synth_op));
-  int sponge = 0, ram = 0, merkle = 0;
+  if (!ops) return -1;
   for (size_t l = 0; l < levels; l++) {
     synth_op *o = &ops[l];
     if (l >= n_ops) { o->kind = OP_PAD; continue; }
@@ -630,30 +676,220 @@ int orc_build_trace(const zkl_op *zops, uint32_t n_ops, const uint8_t pid[32], c
       if (z->regs[i] > 7) { free(ops); return -1; }
       o->abs_regs[i] = z->regs[i];
     }
-    sponge |= o->kind == OP_ABSORB || o->kind == OP_SQUEEZE;
-    ram |= o->kind == OP_LOAD || o->kind == OP_STORE;
-    merkle |= o->kind == OP_MFIRST || o->kind == OP_MSTEP || o->kind == OP_MLAST;
+    P->sponge |= o->kind == OP_ABSORB || o->kind == OP_SQUEEZE;
+    P->ram |= o->kind == OP_LOAD || o->kind == OP_STORE;
+    P->merkle |= o->kind == OP_MFIRST || o->kind == OP_MSTEP || o->kind == OP_MLAST;
   }
-  zk_cols c;
-  cols_for_config(1, ram, sponge, merkle, 1, &c);
-  if (width_out) *width_out = (uint32_t)c.width;
-  if (n_rows_out) *n_rows_out = (uint32_t)(levels * 32);
-  if (!t) { free(ops); return 0; }
-  fe slots[8];
   uint32_t ns = 0;
   for (uint32_t i = 0; i < n_main; i++) { /* encode_vmarg_to_elements (utils.rs:79-97) */
     const zkl_vm_arg *a = &margs[i];
     int need = a->tag == 2 ? 2 : 1;
     if (a->tag > 2 || ns + need > 8) { free(ops); return -1; }
-    if (a->tag == 0) { uint64_t x; memcpy(&x, a->bytes, 8); slots[ns++] = x; }
-    else { slots[ns++] = be_from_le8(a->bytes); if (a->tag == 2) slots[ns++] = be_from_le8(a->bytes + 16); }
+    if (a->tag == 0) { uint64_t x; memcpy(&x, a->bytes, 8); P->slots[ns++] = x; }
+    else { P->slots[ns++] = be_from_le8(a->bytes); if (a->tag == 2) P->slots[ns++] = be_from_le8(a->bytes + 16); }
   }
-  fe regs0[NR] = {0};
   uint32_t tail = NR - ns;
-  for (uint32_t i = 0; i < n_secret && i < tail; i++) regs0[i] = secret[i];
-  for (uint32_t j = 0; j < ns; j++) regs0[tail + j] = slots[j];
-  int rc = build_core(ops, levels, pid, commit, sponge, ram, merkle, rom0_in ? ((fe)rom0_in->hi << 64 | rom0_in->lo) : 0,
-                      regs0, slots, ns, t, pi);
-  free(ops);
+  for (uint32_t i = 0; i < n_secret && i < tail; i++) P->regs0[i] = secret[i];
+  for (uint32_t j = 0; j < ns; j++) P->regs0[tail + j] = P->slots[j];
+  P->n_slots = ns;
+  P->ops = ops;
+  P->levels = levels;
+  P->n_ops = n_ops;
+  return 0;
+}
+
+/* The op-list trace builder (zkl_build_trace's twin): builder::Op list (builder.rs:25-158)
+ * -> build_full_trace (mod.rs:434-524) over next_pow2(n_ops) levels. */
+int orc_build_trace(const zkl_op *zops, uint32_t n_ops, const uint8_t pid[32], const uint8_t commit[32],
+                    const uint64_t *secret, uint32_t n_secret, const zkl_vm_arg *margs, uint32_t n_main,
+                    const zkl_f128 *rom0_in, zkl_f128 *t, zkl_air_public_inputs *pi, uint32_t *width_out,
+                    uint32_t *n_rows_out) {
+  orc_prog P;
+  if (parse_program(zops, n_ops, secret, n_secret, margs, n_main, &P)) return -1;
+  zk_cols c;
+  cols_for_config(1, P.ram, P.sponge, P.merkle, 1, &c);
+  if (width_out) *width_out = (uint32_t)c.width;
+  if (n_rows_out) *n_rows_out = (uint32_t)(P.levels * 32);
+  int rc = 0;
+  if (t)
+    rc = build_core(P.ops, P.levels, pid, commit, P.sponge, P.ram, P.merkle,
+                    rom0_in ? ((fe)rom0_in->hi << 64 | rom0_in->lo) : 0, P.regs0, P.slots, P.n_slots, t, pi);
+  free(P.ops);
+  return rc;
+}
+
+/* The RAM table of RamTraceBuilder::fill_table (ram.rs:43-271) row by row from row 0: pad rows
+ * (row % 32 >= 29) take the sorted events in order; the other rows between two same-address
+ * events mirror the earlier one.  k: sorted events placed above row r (advanced here). */
+typedef struct { int sorted, shown; fe a, clk, v, w; } ram_cell;
+static ram_cell ram_next_row(size_t r, size_t *k, fe (*srt)[4], size_t n_ev) {
+  ram_cell x;
+  memset(&x, 0, sizeof x);
+  const fe *e = NULL;
+  if (r % 32 >= 29 && *k < n_ev) {
+    e = srt[*k];
+    x.sorted = 1;
+    (*k)++;
+  } else if (r % 32 < 29 && *k > 0 && *k < n_ev && srt[*k - 1][0] == srt[*k][0]) {
+    e = srt[*k - 1];
+  }
+  if (e) { x.shown = 1; x.a = e[0]; x.clk = e[1]; x.v = e[2]; x.w = e[3]; }
+  return x;
+}
+
+/* RamTraceBuilder::fill_table restricted to rows [r0, r1) of an n-row trace: the sums and the
+ * last-write state run from row 0; tw holds the window (m rows, full layout c). */
+static void ram_fill_window(zkl_f128 *tw, size_t r0, size_t r1, size_t n, const zk_cols *c, const uint8_t pid[32],
+                            fe (*ev)[4], size_t n_ev) {
+  size_t m = r1 - r0;
+  fe (*srt)[4] = (fe(*)[4])malloc((n_ev + 1) * sizeof *srt);
+  memcpy(srt, ev, n_ev * sizeof *srt);
+  qsort(srt, n_ev, sizeof *srt, cmp_event);
+  fe fc[2];
+  program_field_commitment(pid, fc);
+  fe q0 = fc[0], q2 = fe_mul(q0, q0), q3 = fe_mul(q2, q0), q4 = fe_mul(q2, q2), q5 = fe_mul(q4, q0);
+  fe r1c = fe_add(q2, 1), r2c = fe_add(q3, q0), r3c = fe_add(q5, 7);
+#define COMPRESS(a, clk, v, w) fe_add(fe_add(fe_add((a), fe_mul(r1c, (clk))), fe_mul(r2c, (v))), fe_mul(r3c, (w)))
+  fe gp = 0, last = 0, gu = 0;
+  size_t k = 0, u = 0; /* sorted events placed; level-order events added to the unsorted sum */
+  ram_cell prev, cur = ram_next_row(0, &k, srt, n_ev);
+  for (size_t r = 0; r < r1; r++) {
+    ram_cell nxt;
+    memset(&nxt, 0, sizeof nxt);
+    if (r + 1 < n) nxt = ram_next_row(r + 1, &k, srt, n_ev);
+    if (r > 0 && prev.sorted) {
+      gp = fe_add(gp, COMPRESS(prev.a, prev.clk, prev.v, prev.w));
+      last = cur.a == prev.a ? fe_add(fe_mul(fe_sub(1, prev.w), last), fe_mul(prev.w, prev.v)) : fe_mul(prev.w, prev.v);
+    }
+    if (r > 0 && (r - 1) % 32 == 28 && u < n_ev && ev[u][1] == (fe)((r - 1) / 32)) {
+      gu = fe_add(gu, COMPRESS(ev[u][0], ev[u][1], ev[u][2], ev[u][3]));
+      u++;
+    }
+    if (r >= r0) {
+      size_t q = r - r0;
+      if (cur.sorted) set_fe(tw, m, c->ram_sorted, q, 1);
+      if (cur.shown) {
+        set_fe(tw, m, c->ram_s_addr, q, cur.a);
+        set_fe(tw, m, c->ram_s_clk, q, cur.clk);
+        set_fe(tw, m, c->ram_s_val, q, cur.v);
+        set_fe(tw, m, c->ram_s_is_write, q, cur.w);
+      }
+      set_fe(tw, m, c->ram_gp_sorted, q, gp);
+      set_fe(tw, m, c->ram_s_last_write, q, last);
+      set_fe(tw, m, c->ram_gp_unsorted, q, gu);
+      if (cur.sorted && r + 1 < n) {
+        set_fe(tw, m, c->eq_inv, q, fe_inv(fe_sub(nxt.a, cur.a)));
+        if (nxt.sorted && nxt.a == cur.a) {
+          fe delta = nxt.clk > cur.clk ? nxt.clk - cur.clk : 0;
+          for (int i = 0; i < 32; i++) set_fe(tw, m, c->gadget_b + i, q, (delta >> i) & 1);
+        }
+      }
+    }
+    prev = cur;
+    cur = nxt;
+  }
+#undef COMPRESS
+  free(srt);
+}
+
+/* compute_segment_feature_mask over the ops of levels [l0, l1) (segment_planner.rs:283-334,
+ * prove.rs:1078-1083) */
+static uint64_t seg_mask(uint64_t base, const synth_op *ops, size_t n_ops, size_t l0, size_t l1) {
+  int sp = 0, rm = 0, mk = 0;
+  for (size_t l = l0; l < l1 && l < n_ops; l++) {
+    int k = ops[l].kind;
+    sp |= k == OP_ABSORB || k == OP_SQUEEZE;
+    rm |= k == OP_LOAD || k == OP_STORE;
+    mk |= k == OP_MFIRST || k == OP_MSTEP || k == OP_MLAST;
+  }
+  uint64_t m = base & (FM_VM | FM_VM_EXPECT);
+  if ((base & FM_RAM) && rm) m |= FM_RAM;
+  if ((base & FM_MERKLE) && mk) m |= FM_MERKLE;
+  if ((base & FM_SPONGE) && sp) m |= FM_SPONGE;
+  if ((base & FM_POSEIDON) && (sp || mk)) m |= FM_POSEIDON;
+  return (m != 0 && m != base) ? m : base;
+}
+
+/* zkl_build_segment_trace's twin: rows [r_start, r_end) of the program's trace in the segment's
+ * layout with its AIR public inputs and VM state hashes (prove.rs:1057-1134, mod.rs:316-380),
+ * built by streaming every level through a 32-row scratch and keeping the window's levels. */
+int orc_build_segment_trace(const zkl_op *zops, uint32_t n_ops, const uint8_t pid[32], const uint8_t commit[32],
+                            const uint64_t *secret, uint32_t n_secret, const zkl_vm_arg *margs, uint32_t n_main,
+                            const zkl_f128 *rom0_in, uint32_t r_start, uint32_t r_end, zkl_f128 *t_out,
+                            zkl_air_public_inputs *pi, uint32_t *width_out, uint8_t state_in[32],
+                            uint8_t state_out[32]) {
+  orc_prog P;
+  if (parse_program(zops, n_ops, secret, n_secret, margs, n_main, &P)) return -1;
+  size_t n = P.levels * 32, m = (size_t)r_end - r_start;
+  if (r_start >= r_end || r_end > n || r_start % 32 || r_end % 32 || (m & (m - 1))) { free(P.ops); return -1; }
+  size_t l0 = r_start / 32, l1 = r_end / 32;
+  zk_cols cf, cs;
+  cols_for_config(1, P.ram, P.sponge, P.merkle, 1, &cf);
+  uint64_t base = FM_VM | (P.sponge ? FM_SPONGE | FM_POSEIDON : 0) | (P.ram ? FM_RAM : 0) |
+                  (P.merkle ? FM_MERKLE | FM_POSEIDON : 0);
+  uint64_t eff = seg_mask(base, P.ops, P.n_ops, l0, l1);
+  int e_ram = !!(eff & FM_RAM), e_mk = !!(eff & FM_MERKLE);
+  cols_for_config(1, e_ram, !!(eff & FM_SPONGE), e_mk, 1, &cs);
+  if (width_out) *width_out = (uint32_t)cs.width;
+  if (!t_out) { free(P.ops); return 0; }
+  pos_suite ps;
+  pos_suite_derive(pid, POS_ROUNDS, &ps);
+  rom_k rk;
+  rom_k_init(pid, &rk);
+  orc_vm vm;
+  zkl_f128 *sc = (zkl_f128 *)malloc((size_t)cf.width * 32 * sizeof(zkl_f128));
+  zkl_f128 *tw = (zkl_f128 *)calloc((size_t)cf.width * m, sizeof(zkl_f128));
+  int rc = vm_init(&vm, P.levels, P.regs0, rom0_in ? ((fe)rom0_in->hi << 64 | rom0_in->lo) : 0);
+  if (!sc || !tw) rc = -1;
+  for (size_t l = 0; !rc && l < P.levels; l++) {
+    memset(sc, 0, (size_t)cf.width * 32 * sizeof(zkl_f128));
+    if (level_fill(sc, 32, 0, l, &P.ops[l], &cf, &ps, pid, &vm)) { rc = -1; break; }
+    level_rom(sc, 32, 0, &cf, &rk, &vm);
+    if (l >= l0 && l < l1)
+      for (int col = 0; col < cf.width; col++)
+        memcpy(tw + (size_t)col * m + (l - l0) * 32, sc + (size_t)col * 32, 32 * sizeof(zkl_f128));
+  }
+  if (!rc) {
+    if (P.ram) ram_fill_window(tw, r_start, r_end, n, &cf, pid, vm.ev, vm.n_ev);
+    /* SegmentLayout::from_full_columns (mod.rs:80-235): the segment's columns by name */
+    for (int col = 0; col < cs.width; col++) {
+      int fcol;
+      if (col < cs.ram_sorted) fcol = col;
+      else if (e_ram && col < cs.ram_sorted + 8) fcol = cf.ram_sorted + (col - cs.ram_sorted);
+      else if (e_mk && col >= cs.merkle_g && col < cs.merkle_g + 7) fcol = cf.merkle_g + (col - cs.merkle_g);
+      else fcol = cf.pi_prog + (col - cs.pi_prog);
+      memcpy(t_out + (size_t)col * m, tw + (size_t)fcol * m, m * sizeof(zkl_f128));
+    }
+    program_pi(&vm, pid, commit, P.sponge, P.ram, P.merkle, P.slots, P.n_slots, pi);
+    pi->segment_feature_mask = eff;
+    put_fe(&pi->pc_init, (fe)l0);
+    if (P.ram) { /* compute_segment_boundary_bytes (prove.rs:1197-1287) */
+      put_fe(&pi->ram_gp_unsorted_in, get_fe(tw, m, cf.ram_gp_unsorted, 0));
+      put_fe(&pi->ram_gp_unsorted_out, get_fe(tw, m, cf.ram_gp_unsorted, m - 1));
+      put_fe(&pi->ram_gp_sorted_in, get_fe(tw, m, cf.ram_gp_sorted, 0));
+      put_fe(&pi->ram_gp_sorted_out, get_fe(tw, m, cf.ram_gp_sorted, m - 1));
+    }
+    for (int i = 0; i < 3; i++) {
+      put_fe(&pi->rom_s_in[i], get_fe(tw, m, cf.rom_s + i, 0));
+      put_fe(&pi->rom_s_out[i], get_fe(tw, m, cf.rom_s + i, m - 32 + 28));
+    }
+    trace_pi(t_out, m, &cs, e_ram, pi);
+    /* vm_state_hash_row_with_layout (utils.rs:312-339) of the segment's first and last rows */
+    for (int which = 0; which < 2; which++) {
+      uint8_t buf[15 + 8 * 16];
+      memcpy(buf, "zkl/vm/state-v1", 15);
+      size_t row = which ? m - 1 : 0;
+      for (int i = 0; i < NR; i++) {
+        fe v = get_fe(t_out, m, cs.r_start + i, row);
+        for (int bb = 0; bb < 16; bb++) buf[15 + 16 * i + bb] = (uint8_t)(v >> (8 * bb));
+      }
+      uint8_t *dst = which ? state_out : state_in;
+      if (dst) orc_blake3(buf, sizeof buf, dst);
+    }
+  }
+  vm_free(&vm);
+  free(sc);
+  free(tw);
+  free(P.ops);
   return rc;
 }

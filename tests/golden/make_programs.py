@@ -6,9 +6,10 @@ examples/fib-2pow16-log-n.zlisp) pinned by the CPU oracle:
     safe-add/safe-sub, hash2, constant def, calls, let; zk-lisp-compiler/src/lower/*.rs) and
     program_id = BLAKE3(file bytes) (zk-lisp-compiler/src/lib.rs:239-245); the source text is not
     copied, only its length and BLAKE3;
-  * for each plan -- the CLI default max segment rows 4096 (the published rollup run: 16
-    segments) and --max-segment-rows 65536 (rollup-bench = one 65,536-row segment, the metric's
-    shape on a real program) -- the segment rows and widths, the oracle's segment proofs (each
+  * for each plan -- --max-segment-rows 1024 (rollup-bench = 64 segments: BASELINE configs[3]'s
+    literal workload, segment_planner.rs:108-113), the CLI default 4096 (the published rollup
+    run: 16 segments) and 65536 (rollup-bench = one 65,536-row segment, the metric's shape on a
+    real program) -- the segment rows and widths, the oracle's segment proofs (each
     checked by the oracle verifier), the zl1 step proofs and the ZKLRC1 aggregation artifact in
     both trace modes (agg_ref trace_mode 0 = valid, what proof.bin holds; 1 = the reference's
     trace: next_pow2(max(children, 8)) rows and hash_row_poseidon root errors, agg/trace.rs:397-398,
@@ -20,7 +21,7 @@ are `let` args, so PublicInputs::main_args = [U64 10, Bytes32 01 00..00]); fib-2
 no arguments.  Defaults q 64, blowup 16, grind 16, 128-bit target (Quadratic aggregation).
 
 Run in the build container (needs /root/reference for the source text; ~10-15 min on 8 threads):
-    python tests/golden/make_programs.py [--threads 8] [--only rollup-bench]
+    python tests/golden/make_programs.py [--threads 8] [--only rollup-bench] [--plans 1024]
 """
 import argparse
 import ctypes as C
@@ -48,7 +49,7 @@ PROGRAMS = {
     "rollup-bench": ([10, 1], [(0, (10).to_bytes(8, "little")), (2, bytes([1]))], []),
     "fib-2pow16-log-n": ([], [], []),
 }
-PLANS = [1 << 12, 1 << 16]
+PLANS = [1 << 10, 1 << 12, 1 << 16]
 CLI = {"queries": 64, "blowup": 16, "grind": 16, "min_security_bits": 128}
 
 
@@ -102,6 +103,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--only", default=None)
+    ap.add_argument("--plans", default=None, help="comma-separated max segment rows (default: all); others kept")
     args = ap.parse_args()
     oracle_lib.set_threads(args.threads)
     res = json.load(open(OUT)) if os.path.exists(OUT) else {}
@@ -116,8 +118,9 @@ def main():
                  "cli": dict(CLI, compile_args=u64_args, main_args=[[tg, bytes(b).hex()] for tg, b in main_args],
                              secret_u64=secret),
                  "schema": [[list(a) for a in schema[0]], schema[1]] if schema else None,
-                 "ops": [[k, f] for k, f in ops], "blocks": [list(b) for b in blocks], "plans": {}}
-        for mr in PLANS:
+                 "ops": [[k, f] for k, f in ops], "blocks": [list(b) for b in blocks],
+                 "plans": dict(res.get(name, {}).get("plans", {}))}
+        for mr in ([int(x) for x in args.plans.split(",")] if args.plans else PLANS):
             print(f" plan max_segment_rows {mr}", flush=True)
             entry["plans"][str(mr)] = prove_plan(pid, ops, main_args, secret, mr,
                                                  log=lambda s: print(s, flush=True))

@@ -225,6 +225,28 @@ def build_trace(ops, program_id: bytes, program_commitment: bytes | None = None,
     return rc, trace, pi, w.value, n.value
 
 
+def build_segment_trace(ops, program_id: bytes, r_start: int, r_end: int, program_commitment: bytes | None = None,
+                        secret_args=(), main_args=None, rom0: int = 0):
+    """orc_build_segment_trace (zkl_build_segment_trace's twin: every level streamed, no full
+    trace).  Returns (rc, trace, AirPublicInputs, W, state_in, state_out)."""
+    commit = bytes(program_commitment if program_commitment is not None else program_id)
+    sec = (C.c_uint64 * max(1, len(secret_args)))(*secret_args)
+    n_main = 0 if main_args is None else len(main_args)
+    ma = None if main_args is None else C.cast(main_args, C.c_void_p)
+    r0 = F128(rom0 & (2 ** 64 - 1), rom0 >> 64)
+    w = C.c_uint32()
+    args = (C.cast(ops, C.c_void_p), C.c_uint32(len(ops)), bytes(program_id), commit, sec, C.c_uint32(len(secret_args)),
+            ma, C.c_uint32(n_main), C.byref(r0), C.c_uint32(r_start), C.c_uint32(r_end))
+    rc = lib().orc_build_segment_trace(*args, None, None, C.byref(w), None, None)
+    if rc != 0:
+        return rc, None, None, 0, None, None
+    trace = (F128 * (w.value * (r_end - r_start)))()
+    pi = AirPublicInputs()
+    sin, sout = (C.c_uint8 * 32)(), (C.c_uint8 * 32)()
+    rc = lib().orc_build_segment_trace(*args, trace, C.byref(pi), C.byref(w), sin, sout)
+    return rc, trace, pi, w.value, bytes(sin), bytes(sout)
+
+
 def default_options(width, n, queries=64, blowup=16, grind=16):
     parts = 16 if n >= 1 << 20 else 8 if n >= 1 << 18 else 4 if n >= 1 << 16 else 2 if n >= 1 << 14 else 1
     rate = 8 if width <= 32 else 16

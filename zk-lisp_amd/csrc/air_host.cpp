@@ -77,7 +77,15 @@ static void rom_weights(uint32_t seed, fe out[59]) {  // utils.rs:95-121
 // program's mask for a narrow trace without comparing widths (vm/air/mod.rs:141-163); only the
 // constraint degrees (composition column count) are used.
 std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n, AirInstance& A, bool check_width) {
-  A = AirInstance{};
+  {  // a fresh instance on the vectors' capacity (a prover context rebuilds it every proof)
+    std::vector<int> db = std::move(A.degree_base), dc = std::move(A.degree_cycle);
+    std::vector<Assertion> as = std::move(A.assertions);
+    A = AirInstance{};
+    db.clear(); dc.clear(); as.clear();
+    A.degree_base = std::move(db);
+    A.degree_cycle = std::move(dc);
+    A.assertions = std::move(as);
+  }
   A.n = n;
   uint64_t eff = pi.segment_feature_mask ? pi.segment_feature_mask : pi.feature_mask;
   bool f_pose = eff & FM_POSEIDON, f_vm = eff & FM_VM, f_exp = eff & FM_VM_EXPECT, f_sponge = eff & FM_SPONGE,
@@ -170,7 +178,8 @@ std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n,
   A.num_comp_cols = (int)((max_eval - (n - 1) + n - 1) / n);
 
   // ---- assertions (ScheduleAir, VM PI, RomAir), dedup by (col, step), Winterfell order
-  std::vector<Assertion> raw;
+  static thread_local std::vector<Assertion> raw;  // scratch kept by the thread (no per-proof heap churn)
+  raw.clear();
   size_t last = n - 1, lvls = n / STEPS;
   if (pi.n_main_slots > ZKL_MAX_MAIN_SLOTS) return "n_main_slots exceeds ZKL_MAX_MAIN_SLOTS";
   fe pc_init = fe_from(pi.pc_init);
@@ -212,7 +221,8 @@ std::string build_air(const zkl_air_public_inputs& pi, uint32_t width, size_t n,
   }
   if (raw.empty()) raw.push_back({(uint32_t)cols.mask, (uint32_t)last, fe_zero()});
   // keep-first dedup by (col, step) then sort by (step, col) -- stable on the key
-  std::vector<size_t> idx(raw.size());
+  static thread_local std::vector<size_t> idx;
+  idx.resize(raw.size());
   for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
   std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
     if (raw[a].step != raw[b].step) return raw[a].step < raw[b].step;

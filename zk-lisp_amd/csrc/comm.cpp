@@ -10,6 +10,7 @@
 // one, e.g. torch's, shares it), so the library loads and the single-GPU path runs without it.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -48,8 +49,16 @@ const Rccl& rccl() {
   static Rccl r;
   static std::once_flag once;
   std::call_once(once, [] {
-    r.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-    if (!r.h) r.h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    // ZKL_RCCL_LIB names another NCCL-ABI library: the tests' shared-memory stub
+    // (tests/stub/nccl_shm_stub.cpp) drives the multi-rank branches below with several
+    // processes on one GPU, which RCCL refuses (duplicate devices)
+    const char* alt = getenv("ZKL_RCCL_LIB");
+    if (alt && *alt) {
+      r.h = dlopen(alt, RTLD_NOW | RTLD_LOCAL);
+    } else {
+      r.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+      if (!r.h) r.h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    }
     if (!r.h) {
       const char* e = dlerror();
       r.err = std::string("RCCL not available: ") + (e ? e : "dlopen failed");

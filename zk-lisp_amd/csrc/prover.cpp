@@ -129,10 +129,14 @@ struct zkl_ctx {
   int ktiming = 1;  // 0: no kernel-family events, 1: trace row hash only, 2: every family
   double kfam_ms[ZKL_NUM_KFAMILIES] = {0};
   int kfam_n[ZKL_NUM_KFAMILIES] = {0};
-  // host scratch kept across proofs (gather plan, proof bytes): no per-proof allocation of the
-  // large host buffers
+  // host scratch kept across proofs (gather plan, proof bytes, the AIR instance with its ~2.9e5
+  // assertions): no per-proof allocation of the large host buffers
   std::vector<uint64_t> addrs_s;
   std::vector<uint8_t> proof_s;
+  AirInstance air;
+  // zkl_hip_trace_buffer: pinned host traces the caller fills in place (two slots: one filled
+  // while the other's proof runs); zkl_hip_prove_segment DMAs columns straight from them
+  HBuf tbuf[ZKL_TRACE_BUFFERS];
 };
 
 static const char* kFamilyNames =
@@ -383,7 +387,12 @@ void upload_trace_chunked(zkl_ctx* C, const void* h_trace, uint32_t W, size_t n,
   const size_t col_bytes = n * sizeof(fe);
   const uint32_t per = (uint32_t)std::max<size_t>(1, C->up_slot_bytes / col_bytes);
   const unsigned nt = up_threads();
-  const bool direct = up_direct();
+  // a trace in one of the context's own pinned buffers (zkl_hip_trace_buffer) is DMA'd in place
+  bool in_tbuf = false;
+  for (const HBuf& b : C->tbuf)
+    in_tbuf |= b.p && (const char*)h_trace >= (const char*)b.p &&
+               (const char*)h_trace + (size_t)W * col_bytes <= (const char*)b.p + b.bytes;
+  const bool direct = in_tbuf || up_direct();
   bool used[UP_SLOTS] = {false, false, false, false};
   double copy_ms = 0, wait_ms = 0;
   auto ms_since = [](std::chrono::steady_clock::time_point a) {
@@ -417,7 +426,7 @@ void upload_trace_chunked(zkl_ctx* C, const void* h_trace, uint32_t W, size_t n,
   C->up_ms = ms_since(t0);
   if (getenv("ZKL_UP_DEBUG"))
     fprintf(stderr, "[zkl upload] %u cols x %zu rows: loop %.2f ms (host copy %.2f ms on %u threads, slot waits %.2f ms)%s\n",
-            W, n, C->up_ms, copy_ms, nt, wait_ms, direct ? " direct" : "");
+            W, n, C->up_ms, copy_ms, nt, wait_ms, in_tbuf ? " pinned trace buffer" : direct ? " direct" : "");
 }
 
 // proofs running in any context: the row-digest rule (a process-wide test switch, DESIGN.md
@@ -515,7 +524,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   coin.counter = 0;  // coin.seed is on the device until the constraint root
   // The AIR instance (layout, degrees, ~2.9e5 assertions at n = 2^16) is built on the host
   // meanwhile too.
-  AirInstance air;
+  AirInstance& air = C->air;
   {
     std::string e = build_air(pi, W, n, air);
     if (e.empty() && o.blowup_factor < (uint32_t)air.ce_blowup) e = "blowup factor below constraint-evaluation blowup";
@@ -1055,38 +1064,65 @@ int zkl_hip_init(int device, zkl_ctx** out) {
     HIPCHECK(hipGetDeviceCount(&cnt));
     if (device < 0 || device >= cnt) throw InvalidArg("no such HIP device");
     HIPCHECK(hipSetDevice(device));
-    // The transcript's host round trips wait on short device tails; a blocking (interrupt)
-    // wait there was seen to wake 20-30 ms late on some boxes.  Spin-waiting costs one host core
-    // per waiting context.  ZKL_SPIN=0 keeps the runtime's default; the flag only takes effect
-    // before the device's primary context exists, later calls fail harmlessly.
-    {
-      static std::once_flag once;
-      std::call_once(once, [] {
-        const char* e = getenv("ZKL_SPIN");
-        if (!(e && !strcmp(e, "0"))) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
-        (void)hipGetLastError();
-        // Host memory handed back to the kernel (munmap, heap trim) while a proof runs was
-        // followed by 10-30 ms of idle GPU in ~1 proof of 3 (the driver updates the process's GPU
-        // mappings and stops its queues meanwhile).  glibc returns memory on
-        // free() of blocks above its (dynamic) mmap threshold and when the free heap top
-        // exceeds the trim threshold, so the process keeps what it allocated instead: blocks
-        // below 32 MiB (glibc's largest mmap threshold) come from the heap, the heap grows in
-        // 64 MiB steps and is not trimmed until 2 GiB of its top are free.  Measured: 3 of 3
-        // processes with stalled proofs under glibc's defaults, 0 of 3 with the heap kept
-        // (profiles/r04/stalls.md).  ZKL_MALLOC_TUNE=0 keeps glibc's defaults.
-        const char* m = getenv("ZKL_MALLOC_TUNE");
-        if (!(m && !strcmp(m, "0"))) {
-          (void)mallopt(M_MMAP_THRESHOLD, 32 << 20);
-          (void)mallopt(M_TOP_PAD, 64 << 20);
-          (void)mallopt(M_TRIM_THRESHOLD, 0x7fffffff);
-        }
-      });
-    }
     auto* c = new zkl_ctx();
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete c; throw DeviceError(hipGetErrorString(e)); }
     *out = c;
+  });
+}
+
+// Process-level settings are the embedding application's decision, so zkl_hip_init changes
+// nothing outside the library; this call applies them on request (include/zkl_hip.h).
+int zkl_hip_process_tuning(uint32_t flags, uint32_t* applied) {
+  if (applied) *applied = 0;
+  if (flags & ~(uint32_t)(ZKL_TUNE_SPIN | ZKL_TUNE_MALLOC)) return ZKL_E_INVALID;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  uint32_t ok = 0;
+  if (flags & ZKL_TUNE_SPIN) {
+    // The transcript's host round trips wait on short device tails; a blocking (interrupt) wait
+    // there was seen to wake 20-30 ms late on some boxes.  Spin-waiting costs one host core per
+    // waiting context.  The flag is per device and only takes effect before the device's primary
+    // context exists: every visible device gets it, and it counts as applied only if all took it.
+    int cnt = 0, cur = 0;
+    bool all = hipGetDeviceCount(&cnt) == hipSuccess && cnt > 0 && hipGetDevice(&cur) == hipSuccess;
+    for (int d = 0; all && d < cnt; d++)
+      all = hipSetDevice(d) == hipSuccess && hipSetDeviceFlags(hipDeviceScheduleSpin) == hipSuccess;
+    if (cnt > 0) (void)hipSetDevice(cur);
+    (void)hipGetLastError();
+    if (all) ok |= ZKL_TUNE_SPIN;
+  }
+  if (flags & ZKL_TUNE_MALLOC) {
+    // Host memory handed back to the kernel (munmap, heap trim) while a proof runs was followed
+    // by 10-30 ms of idle GPU in ~1 proof of 3 in round 4 (profiles/r04/stalls.md).
+    // glibc returns memory on free() of blocks above its (dynamic) mmap threshold and when the
+    // free heap top exceeds the trim threshold; with these settings the process keeps what it
+    // allocated: blocks below 32 MiB come from the heap, the heap grows in 64 MiB steps and is not
+    // trimmed until 2 GiB of its top are free.
+    if (mallopt(M_MMAP_THRESHOLD, 32 << 20) == 1 && mallopt(M_TOP_PAD, 64 << 20) == 1 &&
+        mallopt(M_TRIM_THRESHOLD, 0x7fffffff) == 1)
+      ok |= ZKL_TUNE_MALLOC;
+  }
+  if (applied) *applied = ok;
+  return ok == flags ? ZKL_OK : ZKL_E_DEVICE;
+}
+
+int zkl_hip_trace_buffer(zkl_ctx* c, uint32_t slot, size_t bytes, zkl_f128** out) {
+  if (!c || !out || !bytes || slot >= ZKL_TRACE_BUFFERS) return ZKL_E_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  *out = nullptr;
+  return run_guarded(c, [&] {
+    HIPCHECK(hipSetDevice(c->device));
+    HBuf& b = c->tbuf[slot];
+    if (bytes > b.bytes) {  // exact size: one segment shape is the common case
+      if (b.p) HIPCHECK(hipHostFree(b.p));
+      b.p = nullptr;
+      b.bytes = 0;
+      HIPCHECK(hipHostMalloc(&b.p, bytes, hipHostMallocDefault));
+      b.bytes = bytes;
+    }
+    *out = (zkl_f128*)b.p;
   });
 }
 

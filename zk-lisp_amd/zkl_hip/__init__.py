@@ -163,6 +163,13 @@ def load_library():
     lib.zkl_slice_segment.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, P(AirPublicInputs),
                                       C.c_uint32, C.c_uint32, C.c_void_p, P(AirPublicInputs), P(C.c_uint32),
                                       C.c_void_p, C.c_void_p]
+    lib.zkl_hip_process_tuning.argtypes = [C.c_uint32, P(C.c_uint32)]
+    lib.zkl_hip_trace_buffer.argtypes = [C.c_void_p, C.c_uint32, C.c_size_t, P(C.c_void_p)]
+    lib.zkl_program_new.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                    C.c_uint32, P(F128), P(C.c_void_p), P(C.c_uint32), P(C.c_uint32)]
+    lib.zkl_build_segment_trace.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, P(AirPublicInputs),
+                                            P(C.c_uint32), C.c_void_p, C.c_void_p]
+    lib.zkl_program_free.argtypes = [C.c_void_p]
     lib.zkl_agg_prove.argtypes = [P(C.c_char_p), P(C.c_size_t), C.c_uint32, P(AggOptions), P(P(C.c_uint8)),
                                   P(C.c_size_t), C.c_void_p]
     lib.zkl_agg_verify.argtypes = [C.c_char_p, C.c_size_t, C.c_uint32]
@@ -542,6 +549,20 @@ class Comm:
             self.ptr = C.c_void_p()
 
 
+TUNE_SPIN, TUNE_MALLOC = 1, 2
+
+
+def process_tuning(spin: bool = False, malloc: bool = False) -> dict:
+    """zkl_hip_process_tuning: the opt-in process-wide settings (include/zkl_hip.h; zkl_hip_init
+    changes nothing outside the library).  spin must come before the first Context of the
+    process.  Returns {"spin": bool, "malloc": bool} of what took effect."""
+    lib = load_library()
+    flags = (TUNE_SPIN if spin else 0) | (TUNE_MALLOC if malloc else 0)
+    got = C.c_uint32()
+    lib.zkl_hip_process_tuning(flags, C.byref(got))
+    return {"spin": bool(got.value & TUNE_SPIN), "malloc": bool(got.value & TUNE_MALLOC)}
+
+
 class Context:
     """One prover context per device (zkl_hip_init)."""
 
@@ -581,6 +602,16 @@ class Context:
         rc = self.lib.zkl_hip_prove_segment(self.ptr, ptr, width, n_rows, C.byref(pi), C.byref(opts),
                                             C.byref(out), C.byref(ln))
         return self._finish(rc, out, ln)
+
+    def trace_buffer(self, nbytes: int, slot: int = 0) -> int:
+        """zkl_hip_trace_buffer: address of the context's pinned host trace buffer `slot` (0/1,
+        >= nbytes), to be filled in place and passed to prove_segment (DMA'd without a staging
+        copy)."""
+        p = C.c_void_p()
+        rc = self.lib.zkl_hip_trace_buffer(self.ptr, slot, nbytes, C.byref(p))
+        if rc:
+            self._err(rc)
+        return p.value
 
     def prove_segment_device(self, d_trace_ptr: int, width: int, n_rows: int, pi, opts) -> bytes:
         """Same with the trace already resident in HBM (device pointer, e.g. torch data_ptr())."""
@@ -813,3 +844,64 @@ def slice_segment(full, width: int, n_rows: int, ops, pi: AirPublicInputs, r_sta
     if rc:
         raise ZklError(rc, "slice_segment: invalid segment")
     return t, spi, w.value, bytes(sin), bytes(sout)
+
+
+class Program:
+    """A program executed once for per-segment trace building (zkl_program_new): what
+    prove_segment's input side gives (prove.rs:1057-1134 over build_full_trace + slice,
+    vm/trace/mod.rs:316-524) segment by segment, without the full trace in memory.
+    `segment(r_start, r_end)` -> (trace, pi, width, state_in_hash, state_out_hash), bit for bit
+    slice_segment(build_trace(..)); `width` / `n_rows` are the full trace's shape."""
+
+    def __init__(self, ops, program_id: bytes, program_commitment: bytes | None = None, secret_args=(),
+                 main_args=(), rom0: int = 0):
+        self.lib = load_library()
+        arr = (ZklOp * len(ops))(*ops)
+        commit = bytes(program_commitment if program_commitment is not None else program_id)
+        sec = (C.c_uint64 * max(1, len(secret_args)))(*secret_args)
+        ma = _vm_args(list(main_args))
+        r0 = F128(rom0 & (2 ** 64 - 1), rom0 >> 64)
+        w, n = C.c_uint32(), C.c_uint32()
+        self.ptr = C.c_void_p()
+        rc = self.lib.zkl_program_new(C.cast(arr, C.c_void_p), len(ops), bytes(program_id), commit,
+                                      C.cast(sec, C.c_void_p), len(secret_args), C.cast(ma, C.c_void_p),
+                                      len(main_args), C.byref(r0), C.byref(self.ptr), C.byref(w), C.byref(n))
+        if rc != 0:
+            raise ZklError(rc, "Program: invalid program")
+        self.width, self.n_rows, self.n_ops = w.value, n.value, len(ops)
+
+    def segment_width(self, r_start: int, r_end: int) -> int:
+        w = C.c_uint32()
+        rc = self.lib.zkl_build_segment_trace(self.ptr, r_start, r_end, None, None, C.byref(w), None, None)
+        if rc:
+            raise ZklError(rc, "build_segment_trace: invalid segment")
+        return w.value
+
+    def segment_into(self, r_start: int, r_end: int, out_ptr: int):
+        """Writes the segment trace to out_ptr (host memory of width x rows f128):
+        (pi, width, state_in_hash, state_out_hash)."""
+        w = C.c_uint32()
+        spi = AirPublicInputs()
+        sin, sout = (C.c_uint8 * 32)(), (C.c_uint8 * 32)()
+        rc = self.lib.zkl_build_segment_trace(self.ptr, r_start, r_end, C.c_void_p(out_ptr), C.byref(spi),
+                                              C.byref(w), sin, sout)
+        if rc:
+            raise ZklError(rc, "build_segment_trace: invalid segment")
+        return spi, w.value, bytes(sin), bytes(sout)
+
+    def segment(self, r_start: int, r_end: int):
+        w = self.segment_width(r_start, r_end)
+        t = (F128 * (w * (r_end - r_start)))()
+        spi, w, sin, sout = self.segment_into(r_start, r_end, C.addressof(t))
+        return t, spi, w, sin, sout
+
+    def close(self):
+        if self.ptr:
+            self.lib.zkl_program_free(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

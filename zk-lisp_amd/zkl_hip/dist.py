@@ -85,7 +85,8 @@ def rccl_required():
     """True when the hand-off must run over RCCL: more than one rank, each on its own GPU
     (ZKL_BENCH_DEVICE unset) and no explicit ZKL_COMM=gloo.  Same-device rehearsals
     (ZKL_BENCH_DEVICE pins every rank to one GPU, which RCCL refuses as a duplicate device) and
-    the explicit opt-out keep the gloo transport, labelled as such in the bench line."""
+    the explicit opt-out keep the gloo transport, labelled as such in the bench line; a
+    same-device rehearsal with ZKL_RCCL_LIB (the tests' NCCL-ABI stub) runs the RCCL code path."""
     _, world, _ = env()
     return world > 1 and os.environ.get("ZKL_BENCH_DEVICE") is None and os.environ.get("ZKL_COMM", "rccl") != "gloo"
 
@@ -124,7 +125,7 @@ def init_rccl(device, required=None, timeout_s=180.0):
     err, uid = None, None
     if os.environ.get("ZKL_COMM", "rccl") == "gloo":
         err = "ZKL_COMM=gloo"
-    elif world > 1 and os.environ.get("ZKL_BENCH_DEVICE") is not None:
+    elif world > 1 and os.environ.get("ZKL_BENCH_DEVICE") is not None and not os.environ.get("ZKL_RCCL_LIB"):
         err = "same-device rehearsal (ZKL_BENCH_DEVICE pins every rank to one GPU; RCCL needs one GPU per rank)"
     # every rank must be able to enter ncclCommInitRank, or none does (it is collective)
     avail = gather_to_root(err or zkl_hip.comm_available())
@@ -181,12 +182,20 @@ def unpack_blobs(buf):
     return out
 
 
+def gather_timeout_s():
+    """Seconds the RCCL step-proof gather may take once every rank has entered it
+    (ZKL_GATHER_TIMEOUT_S, default 300)."""
+    return float(os.environ.get("ZKL_GATHER_TIMEOUT_S", "300"))
+
+
 def gather_step_bytes(step_bytes, comm=None):
     """Every rank's step encodings on rank 0 (list per rank), None elsewhere: over RCCL when a
-    communicator is given, else over gloo (host bytes)."""
+    communicator is given, else over gloo (host bytes).  The ranks meet at a gloo barrier first,
+    so the watchdog times the transfer itself, not a slower rank's proving."""
     if comm is not None:
         _, world, _ = env()
-        wd = _watchdog(300.0, "the RCCL step-proof gather") if world > 1 else None
+        barrier()
+        wd = _watchdog(gather_timeout_s(), "the RCCL step-proof gather") if world > 1 else None
         try:
             got = comm.gather_bytes(pack_blobs(step_bytes), root=0)
         finally:
