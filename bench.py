@@ -513,20 +513,41 @@ def program_sharded(zkl_hip, dist, device, rank, world, name, max_rows, inflight
                        "step_bytes": sum(d["bytes"] for d in steps)}}
     if res_line is not None:
         out["resident"] = res_line
-    raw = [d["raw"] for d in steps]
+    out["aggregation"] = program_aggregation(zkl_hip, [d["raw"] for d in steps], aggs.get(max_rows, {}))
+    return out
+
+
+def program_aggregation(zkl_hip, raw, gold):
+    """The aggregation over a program's gathered steps (valid trace mode, then verified), checked
+    against the oracle's artifacts where the goldens hold them.  A batch the valid mode must refuse
+    (tests/golden/programs.json "rejected": rollup-bench at 1024 rows cuts its sorted RAM table,
+    DESIGN.md §10) is refused here too, and the reference trace mode's artifact is compared."""
+    a = {"children": len(raw)}
+    want = gold.get("valid", {})
     try:
         t1 = time.perf_counter()
-        art, dg = zkl_hip.agg_prove(raw)
-        a = {"children": len(raw), "ms": round((time.perf_counter() - t1) * 1e3, 1), "artifact_bytes": len(art)}
+        art, _ = zkl_hip.agg_prove(raw)
+        a.update(ms=round((time.perf_counter() - t1) * 1e3, 1), artifact_bytes=len(art))
         zkl_hip.agg_verify(art)
         a["verified"] = True
-        want = aggs.get(max_rows, {}).get("valid")
-        if want:
+        if "sha256" in want:
             a["golden"] = "match" if hashlib.sha256(art).hexdigest() == want["sha256"] else "MISMATCH"
-        out["aggregation"] = a
-    except Exception as e:  # reported in the line, and the run exits non-zero
-        out["aggregation"] = {"error": str(e)}
-    return out
+        elif "rejected" in want:
+            a["golden"] = "MISMATCH"
+            a["error"] = "the valid mode accepted a batch the oracle rejects"
+    except Exception as e:  # noqa: BLE001
+        if "rejected" not in want:
+            return {"error": str(e)}
+        a["valid_mode"] = f"rejected, as by the oracle: {e}"
+    ref = gold.get("reference_trace")
+    if ref and "sha256" in ref:
+        t1 = time.perf_counter()
+        art, _ = zkl_hip.agg_prove(raw, trace_mode=zkl_hip.AGG_TRACE_REFERENCE)
+        a["reference_trace"] = {"ms": round((time.perf_counter() - t1) * 1e3, 1), "artifact_bytes": len(art),
+                                "golden": "match" if hashlib.sha256(art).hexdigest() == ref["sha256"] else "MISMATCH"}
+        if a["reference_trace"]["golden"] == "MISMATCH":
+            a["golden"] = "MISMATCH"
+    return a
 
 
 def program_resident(zkl_hip, ctxs, P, plan, idx, builders):

@@ -22,6 +22,10 @@
 //   zkl::Error                   prove::Error (prove.rs:51-60): Backend(String) for prover and
 //                                device failures, RecursionInvalid for a batch the aggregation
 //                                rejects
+//   zkl::Program                 build_trace + build_segment_trace_with_state (vm/trace/mod.rs:
+//                                279-365) for one segment at a time, without the full trace
+//                                (zkl_program_new / zkl_build_segment_trace)
+//   zkl::process_tuning          the opt-in process-wide settings (zkl_hip_process_tuning)
 //
 // Nothing here runs on the GPU by itself: every call goes through libzkl_hip.so.
 #ifndef ZKL_HIP_HPP
@@ -152,6 +156,13 @@ class Device {
   Device& operator=(const Device&) = delete;
   Device(Device&& o) noexcept : ctx_(o.ctx_) { o.ctx_ = nullptr; }
   zkl_ctx* ctx() const { return ctx_; }
+  // pinned host trace buffer `slot` (0 / 1) of this device context, at least `bytes`: fill it (e.g.
+  // Program::build_segment_into) and prove it with ZkProver::prove_host -- no staging copy
+  BaseElement* trace_buffer(uint32_t slot, size_t bytes) {
+    zkl_f128* p = nullptr;
+    detail::check(zkl_hip_trace_buffer(ctx_, slot, bytes, &p), ctx_);
+    return p;
+  }
   static int count() {
     int n = 0;
     detail::check(zkl_hip_device_count(&n));
@@ -189,6 +200,14 @@ class ZkProver {
                   dev_->ctx());
     return Proof{detail::take(out, len)};
   }
+  // same with a host trace given as a pointer (e.g. one of the Device's pinned trace buffers)
+  Proof prove_host(const BaseElement* trace, uint32_t width, uint32_t length) const {
+    uint8_t* out = nullptr;
+    size_t len = 0;
+    detail::check(zkl_hip_prove_segment(dev_->ctx(), trace, width, length, &pi_, &opts_.raw(), &out, &len),
+                  dev_->ctx());
+    return Proof{detail::take(out, len)};
+  }
   // same with the trace already resident in HBM (device pointer on this Device)
   Proof prove_device(const void* d_trace, uint32_t width, uint32_t length) const {
     uint8_t* out = nullptr;
@@ -204,6 +223,71 @@ class ZkProver {
   AirPublicInputs pi_;
   Device* dev_;
 };
+
+// The opt-in process-wide settings (ZKL_TUNE_SPIN | ZKL_TUNE_MALLOC, zkl_hip.h): returns the flags
+// that took effect; the spin flag only before the first Device of the process
+inline uint32_t process_tuning(uint32_t flags) {
+  uint32_t applied = 0;
+  (void)zkl_hip_process_tuning(flags, &applied);
+  return applied;
+}
+
+// A compiled program (builder::Op list) run once, then traced segment by segment
+// (prove.rs:1057-1134's input side without the full trace): the segment's trace in its own
+// layout, its AirPublicInputs and the VM state hashes at its first and last rows.
+class Program {
+ public:
+  Program(const std::vector<zkl_op>& ops, const Digest& program_id, const Digest& commitment,
+          const std::vector<uint64_t>& secret_args = {}, const std::vector<zkl_vm_arg>& main_args = {}) {
+    detail::check(zkl_program_new(ops.data(), (uint32_t)ops.size(), program_id.data(), commitment.data(),
+                                  secret_args.empty() ? nullptr : secret_args.data(), (uint32_t)secret_args.size(),
+                                  main_args.empty() ? nullptr : main_args.data(), (uint32_t)main_args.size(), nullptr,
+                                  &p_, &width_, &rows_));
+  }
+  ~Program() { zkl_program_free(p_); }
+  Program(const Program&) = delete;
+  Program& operator=(const Program&) = delete;
+  uint32_t full_width() const { return width_; }
+  uint32_t rows() const { return rows_; }  // 32 * next_pow2(ops)
+  uint32_t segment_width(uint32_t r_start, uint32_t r_end) const {
+    uint32_t w = 0;
+    detail::check(zkl_build_segment_trace(p_, r_start, r_end, nullptr, nullptr, &w, nullptr, nullptr));
+    return w;
+  }
+  struct Segment {
+    AirPublicInputs pi;
+    uint32_t width = 0;
+    Digest state_in{}, state_out{};
+  };
+  // writes rows [r_start, r_end) into `out` (segment_width x (r_end - r_start), column-major)
+  Segment build_segment_into(uint32_t r_start, uint32_t r_end, BaseElement* out) const {
+    Segment s;
+    detail::check(zkl_build_segment_trace(p_, r_start, r_end, out, &s.pi, &s.width, s.state_in.data(),
+                                          s.state_out.data()));
+    return s;
+  }
+  // build_segment_trace_with_state (mod.rs:279-310): (trace, segment info)
+  std::pair<TraceTable, Segment> build_segment_trace_with_state(uint32_t r_start, uint32_t r_end) const {
+    TraceTable t(segment_width(r_start, r_end), r_end - r_start);
+    Segment s = build_segment_into(r_start, r_end, t.data());
+    return {std::move(t), s};
+  }
+
+ private:
+  zkl_program* p_ = nullptr;
+  uint32_t width_ = 0, rows_ = 0;
+};
+
+// WinterfellSegmentPlanner::plan_segments (segment_planner.rs:93-276): [(r_start, r_end)]
+inline std::vector<std::pair<uint32_t, uint32_t>> plan_segments(uint32_t n_ops, uint32_t max_rows) {
+  uint32_t k = 0;
+  detail::check(zkl_plan_segments(n_ops, max_rows, nullptr, nullptr, 0, &k));
+  std::vector<uint32_t> a(k), b(k);
+  detail::check(zkl_plan_segments(n_ops, max_rows, a.data(), b.data(), k, &k));
+  std::vector<std::pair<uint32_t, uint32_t>> out;
+  for (uint32_t i = 0; i < k; i++) out.emplace_back(a[i], b[i]);
+  return out;
+}
 
 // verify_proof (prove.rs:802-941) for one segment proof; throws Error::Backend naming the first
 // failing check

@@ -80,6 +80,47 @@ int run_cpu() {
   meta.segments_total = 1;
   EXPECT(throws_backend([&] { (void)zkl::StepProof::from_inner(s.pi, meta, zkl::Proof{{1, 2, 3}}); }, "truncated"));
   EXPECT(throws_backend([&] { (void)zkl::StepProof{{'Z', 'K', 'L'}}.digest(); }, nullptr));
+  // a program traced segment by segment (Program) equals the full trace cut by the planner:
+  // Const/Add ops over 96 levels -> 128 levels, two segments of 2048 rows
+  {
+    std::vector<zkl_op> ops;
+    for (int i = 0; i < 95; i++) {
+      zkl_op a{};
+      a.kind = i % 2 ? ZKL_OP_ADD : ZKL_OP_CONST;
+      a.dst = (uint8_t)(i % 8);
+      a.a = (uint8_t)((i + 1) % 8);
+      a.b = (uint8_t)((i + 3) % 8);
+      a.imm = 1000u + (uint64_t)i;
+      ops.push_back(a);
+    }
+    zkl_op end{};
+    end.kind = ZKL_OP_END;
+    ops.push_back(end);
+    zkl::Digest pid{};
+    pid[0] = 7;
+    const zkl::Program prog(ops, pid, pid);
+    EXPECT(prog.full_width() == 204 && prog.rows() == 4096);
+    const auto plan = zkl::plan_segments((uint32_t)ops.size(), 2048);
+    EXPECT(plan.size() == 2 && plan[1].first == 2048);
+    std::vector<zkl_f128> full((size_t)prog.full_width() * prog.rows());
+    zkl_air_public_inputs fpi{};
+    uint32_t fw = 0, fn = 0;
+    zkl::detail::check(zkl_build_trace(ops.data(), (uint32_t)ops.size(), pid.data(), pid.data(), nullptr, 0, nullptr, 0,
+                                       nullptr, full.data(), &fpi, &fw, &fn));
+    for (const auto& seg : plan) {
+      const auto got = prog.build_segment_trace_with_state(seg.first, seg.second);
+      std::vector<zkl_f128> want((size_t)got.first.width() * got.first.length());
+      zkl_air_public_inputs wpi{};
+      uint32_t ww = 0;
+      zkl::Digest win{}, wout{};
+      zkl::detail::check(zkl_slice_segment(full.data(), fw, fn, ops.data(), (uint32_t)ops.size(), &fpi, seg.first,
+                                           seg.second, want.data(), &wpi, &ww, win.data(), wout.data()));
+      EXPECT(ww == got.first.width() && std::memcmp(want.data(), got.first.data(), want.size() * 16) == 0);
+      EXPECT(std::memcmp(&wpi, static_cast<const zkl_air_public_inputs*>(&got.second.pi), sizeof wpi) == 0);
+      EXPECT(win == got.second.state_in && wout == got.second.state_out);
+    }
+    EXPECT(throws_backend([&] { (void)prog.segment_width(16, 48); }, nullptr));
+  }
   // no device here: the context fails with Error::Backend, not a crash
   int devs = 0;
   if (zkl_hip_device_count(&devs) != ZKL_OK || devs == 0) EXPECT(throws_backend([] { zkl::Device d(0); }, nullptr));
@@ -95,6 +136,10 @@ int run_gpu(const char* out_path) {
   zkl::Device dev(0);
   const zkl::ZkProver prover(opts, s.pi, dev);  // ZkProver::new(options, pub_inputs, rom_acc)
   const zkl::Proof proof = prover.prove(s.trace);
+  // the same trace from the device's pinned trace buffer (no staging copy) gives the same bytes
+  zkl::BaseElement* tb = dev.trace_buffer(1, (size_t)w * n * sizeof(zkl::BaseElement));
+  std::memcpy(tb, s.trace.data(), (size_t)w * n * sizeof(zkl::BaseElement));
+  EXPECT(prover.prove_host(tb, w, n).bytes == proof.bytes);
   zkl::verify_proof(proof, s.pi, opts);
   // a corrupted proof is rejected by the verifier with Error::Backend
   zkl::Proof bad = proof;

@@ -61,6 +61,31 @@ def test_grinding_windows_match_oracle(oracle, gpu_ctx):
         assert got == want, f"seed {seed:#x}"
 
 
+@pytest.mark.parametrize("first", [1, 3, 64])
+def test_grinding_host_continuation_matches_oracle(oracle, gpu_ctx, monkeypatch, first):
+    """when the first four device windows hold no nonce (probability e^-8 at the
+    default window size), the host continues the search window by window and derives the query
+    seed itself (merge_with_int, prover.cpp).  ZKL_TEST_GRIND_FIRST shrinks the first window to
+    `first` tries so the first pass (first * 8 tries) misses at grind 10 and the continuation
+    runs; the proof must still equal the oracle's sequential search."""
+    import zkl_hip
+    oracle.set_threads(1)
+    monkeypatch.setenv("ZKL_TEST_GRIND_FIRST", str(first))
+    n = 1 << 6
+    past = 0
+    for k in range(3):
+        seed = 0x6B1E0000 + k
+        t, pi, w = zkl_hip.synth_vm_segment(seed, 6)
+        opts = zkl_hip.proof_options(w, n, queries=16, blowup=16, grind=10)
+        got = gpu_ctx.prove_segment(t, w, n, pi, opts)
+        ot, opi, _ = oracle.synth_segment(seed, 6)
+        want = oracle.prove(ot, w, n, opi, oracle.ProofOptions(*[getattr(opts, f) for f, _ in opts._fields_]))
+        assert got == want, f"seed {seed:#x}"
+        past += int.from_bytes(got[-8:], "little") > first * 8  # Proof::to_bytes ends with the nonce
+        zkl_hip.verify_segment(got, pi, opts)
+    assert past > 0  # the host continuation found at least one of the nonces
+
+
 @pytest.mark.parametrize("log_n,q,blowup,grind", [
     (5, 8, 16, 0), (6, 32, 8, 4), (8, 64, 16, 10), (10, 64, 16, 12), (7, 255, 8, 1),
 ])

@@ -240,13 +240,19 @@ def test_rollup_first_segment_oracle_proof_matches_golden(oracle):
 
 # ------------------------------------------------------------------ GPU: the whole `prove`
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,max_rows", [("rollup-bench", 4096), ("rollup-bench", 65536),
+@pytest.mark.parametrize("name,max_rows", [("rollup-bench", 4096), ("rollup-bench", 65536), ("rollup-bench", 1024),
                                            ("fib-2pow16-log-n", 4096), ("fib-2pow16-log-n", 65536)])
 def test_program_prove_chain_on_gpu(name, max_rows, gpu_ctx):
     """`zk-lisp prove` of the example with every segment proved on the GPU: segment proofs and
     zl1 steps equal the oracle goldens, the product verifier accepts each proof, and the ZKLRC1
     aggregation over the steps equals the golden in both trace modes (the valid artifact also
-    verifies)."""
+    verifies).  rollup-bench at --max-segment-rows 1024 is BASELINE configs[3]'s 64 segments
+    (segment_planner.rs:108-113); its valid-mode aggregation is refused, as by the oracle: the
+    sorted RAM table crosses the cuts and each segment's ram_gp_sorted_out (its last row,
+    prove.rs:1224-1227) misses the sorted row there that the next segment's ram_gp_sorted_in
+    counts (agg/trace.rs:515-521), so no valid ZlAggAir trace exists."""
+    if str(max_rows) not in G[name]["plans"]:
+        pytest.skip(f"no {max_rows}-row plan goldens")
     g = G[name]["plans"][str(max_rows)]
     _, plan, segs = _segments(name, max_rows)
     assert [list(p) for p in plan] == [s["rows"] for s in g["segments"]]
@@ -262,9 +268,14 @@ def test_program_prove_chain_on_gpu(name, max_rows, gpu_ctx):
         assert sha(steps[-1]) == want["step_sha256"]
     c = G[name]["cli"]
     for mode, key in ((zkl_hip.AGG_TRACE_VALID, "valid"), (zkl_hip.AGG_TRACE_REFERENCE, "reference_trace")):
+        want = g["aggregation"][key]
+        if "rejected" in want:
+            with pytest.raises(zkl_hip.ZklError, match="ZlAggAir"):
+                zkl_hip.agg_prove(steps, queries=c["queries"], blowup=c["blowup"], grind=c["grind"],
+                                  min_security_bits=c["min_security_bits"], trace_mode=mode)
+            continue
         art, dg = zkl_hip.agg_prove(steps, queries=c["queries"], blowup=c["blowup"], grind=c["grind"],
                                     min_security_bits=c["min_security_bits"], trace_mode=mode)
-        want = g["aggregation"][key]
         assert (len(art), sha(art), dg.hex()) == (want["len"], want["sha256"], want["recursion_digest"]), key
         if mode == zkl_hip.AGG_TRACE_VALID:
             zkl_hip.agg_verify(art)

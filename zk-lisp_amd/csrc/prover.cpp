@@ -839,6 +839,9 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   // 4 e^-4) windows = 1.7 instead of the 2.6 of one 2^(g+1) window first and doubling after it.
   // grinding factor 0: the first candidate, nonce 1.
   uint32_t batch = 1u << std::min<uint32_t>(std::max<uint32_t>(o.grinding_factor, 14), 22);
+  // test-only: ZKL_TEST_GRIND_FIRST=<tries> shrinks the first window, so a test reaches the host
+  // continuation below (a path real proofs take with probability e^-8) and checks its nonce
+  if (const char* e = getenv("ZKL_TEST_GRIND_FIRST")) batch = (uint32_t)std::max(1L, std::min(atol(e), 1L << 22));
   uint64_t base = 1;
   auto queue_windows = [&](const fe* d_seed, fe h_seed) {
     *hbest = o.grinding_factor == 0 ? 1ull : ~0ull;
