@@ -162,3 +162,27 @@ def test_ntt_mode_switch_bounds():
         assert lib.zkl_hip_set_ntt_mode(-1) == -1
     finally:
         lib.zkl_hip_set_ntt_mode(1)
+
+
+# Kernels allowed a private segment (scratch), each measured faster than its scratch-free form:
+# the constraint evaluators at 3 waves per SIMD spill (1.57 -> 1.40 ms per headline proof,
+# DESIGN.md §5; 3.42 -> 3.33 ms of Poseidon-block evaluation per rollup-bench proof,
+# profiles/r04/ab_cepose.json), and the Poseidon-block part keeps a stack object at any occupancy.
+# The runtime allocates a queue's scratch at the first dispatch that needs it and keeps it; the
+# round-4 stall study found scratch settings irrelevant (profiles/r04/stalls.md, "scr1").
+SCRATCH_ALLOWED = ("constraint_eval_kernel", "constraint_eval_pose_kernel", "constraint_eval_pose_part_kernel")
+
+
+def test_only_listed_kernels_need_scratch():
+    """every kernel of the shipped library is scratch-free except the listed
+    evaluator kernels (read from the device code objects' metadata, tools/kernel_resources.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from kernel_resources import kernel_resources
+    import zkl_hip
+    res = kernel_resources(zkl_hip.LIB_PATH)
+    assert len(res) > 40, "device code objects not found"
+    bad = [k for k, v in res.items() if (v.get("scratch") or v.get("spill")) and
+           not any(a in k for a in SCRATCH_ALLOWED)]
+    assert not bad, bad
+    assert all(v.get("scratch", 0) == 0 for k, v in res.items() if "pm_kernel" in k or "ntt" in k or "deep" in k)

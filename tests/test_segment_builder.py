@@ -107,3 +107,29 @@ def test_rejections():
     with pytest.raises(zkl_hip.ZklError):
         zkl_hip.Program([zkl_hip.op("SAbsorbN", regs=[0] * 10), zkl_hip.op("SAbsorbN", regs=[1]),
                          zkl_hip.op("End")], pid)  # push_absorb: more than 10 pending (vm.rs:925-935)
+
+
+def test_rollup_1024_sorted_ram_chain_breaks_where_the_table_is_cut():
+    """Why the 64-segment plan's valid-mode aggregation is refused (tests/golden/programs.json
+    "rejected"): compute_segment_boundary_bytes takes ram_gp_sorted at a segment's
+    first and last rows (prove.rs:1224-1227) and the aggregation chains out(i) -> in(i+1)
+    (agg/trace.rs:515-521).  The sorted grand product counts a sorted row on the row after it, so
+    where the cut falls inside the sorted table (the last row of a level is a sorted row) in(i+1)
+    exceeds out(i) by exactly that row's compression; below the table the chain holds."""
+    import oracle_lib
+    ops, pid, secret, ma = _prog("rollup-bench")
+    P = zkl_hip.Program(ops, pid, secret_args=secret, main_args=ma)
+    plan = zkl_hip.plan_segments(len(ops), 1 << 10)
+    n_events = sum(k in ("Load", "Store") for k, _ in G["rollup-bench"]["ops"])
+    fe = lambda f: f.lo | (f.hi << 64)  # noqa: E731
+    breaks = []
+    for i in range(len(plan) - 1):
+        _, a, _, _, _ = P.segment(*plan[i])
+        _, b, _, _, _ = P.segment(*plan[i + 1])
+        diff = oracle_lib.fe_sub(fe(b.ram_gp_sorted_in), fe(a.ram_gp_sorted_out))
+        assert (fe(b.ram_gp_unsorted_in), fe(b.rom_s_in[0])) == (fe(a.ram_gp_unsorted_out), fe(a.rom_s_out[0]))
+        if diff:
+            breaks.append(i)
+    # cuts after segment i lie inside the table while event 3 * 32 * (i + 1) - 1 exists
+    assert breaks == [i for i in range(len(plan) - 1) if 96 * (i + 1) <= n_events]
+    assert breaks  # the published 16 x 4096 plan keeps the table inside segment 0; this one does not

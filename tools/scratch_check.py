@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Per-kernel scratch / VGPR / spill report of a HIP translation unit (hipcc
--Rpass-analysis=kernel-resource-usage).  The product kernels must need no scratch: a kernel with a
-private segment makes the runtime allocate the queue's scratch memory on dispatch.
+-Rpass-analysis=kernel-resource-usage).  Product kernels need no scratch (a kernel with a private
+segment makes the runtime allocate the queue's scratch memory on dispatch) except the
+constraint evaluators listed in tests/test_abi.py (SCRATCH_ALLOWED), which checks the shipped
+library with tools/kernel_resources.py.
 
     python tools/scratch_check.py zk-lisp_amd/csrc/kernels.hip [extra hipcc flags]
 """

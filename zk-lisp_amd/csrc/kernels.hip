@@ -753,7 +753,10 @@ __device__ __forceinline__ void constraint_eval_body(const fe* __restrict__ lde,
 
 // The VM-only and RAM / Merkle instances run at CE_WAVES_CFG waves per SIMD; the PoseidonAir
 // block's own kernel at CE_POSE_WAVES_CFG (3: 48 spilled VGPRs, 3.33 against 3.42 ms of
-// evaluation per rollup-bench proof at the compiler's 2, profiles/r04/ab_cepose.json).
+// evaluation per rollup-bench proof at the compiler's 2, profiles/r04/ab_cepose.json).  The
+// evaluator kernels are the library's only ones with a private segment (spills at 3 waves per
+// SIMD, a stack object in the Poseidon block at any occupancy): the listed exceptions of
+// tests/test_abi.py::test_only_listed_kernels_need_scratch.
 #ifndef CE_POSE_WAVES_CFG
 #define CE_POSE_WAVES_CFG 3
 #endif
