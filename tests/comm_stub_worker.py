@@ -6,9 +6,9 @@ the NCCL-ABI shared-memory stub (ZKL_RCCL_LIB) with several processes on one GPU
 scenario "branches": four gathers -- unequal lengths with a zero-length rank, a blob larger than
 the communicator's buffer (capacity growth), a non-zero root, every rank empty -- each checked on
 its root; prints one JSON line; exit 0 / 5 (wrong bytes).
-scenario "fail": one gather under the stub's injected fault (ZKL_NCCL_STUB_FAIL); the gather must
-raise, and a second one must be refused (the communicator is marked broken); exit 7 when both
-happened as expected, 6 otherwise."""
+scenario "fail": one gather under the stub's injected fault (ZKL_NCCL_STUB_FAIL); if it raises, a
+second one must be refused (the communicator is marked broken): exit 7 then, 6 if the second was not
+refused, 0 if the first gather succeeded (a sender whose blob was delivered before the root failed)."""
 import json
 import os
 import sys
@@ -38,9 +38,9 @@ def main():
             comm.gather_bytes(b"x" * 100, root=0)
         except zkl_hip.ZklError as e:
             first = str(e)
-        else:
-            print(json.dumps({"rank": rank, "error": "the gather did not fail"}), flush=True)
-            return 6
+        else:  # a sender whose blob was delivered before the root failed completes its gather
+            print(json.dumps({"rank": rank, "first": None}), flush=True)
+            return 0
         try:
             comm.gather_bytes(b"y", root=0)
         except zkl_hip.ZklError as e:

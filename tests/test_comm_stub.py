@@ -80,13 +80,15 @@ def test_gather_branches_multi_rank(world):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("op,rank", [("send", 1), ("recv", 0), ("allgather", 0)])
-def test_failed_collective_breaks_the_communicator_on_every_rank(op, rank):
-    """An injected fault in one rank's send / receive / all-gather: that rank's gather fails at
-    once, the peer's fails when its wait runs out; both communicators are then marked broken (a
-    second gather is refused) and both processes exit non-zero."""
+@pytest.mark.parametrize("op,rank,want", [("send", 1, (7, 7)), ("allgather", 0, (7, 7)), ("recv", 0, (7, 0))])
+def test_failed_collective_breaks_the_communicator(op, rank, want):
+    """An injected fault in one rank's send / all-gather / receive: that rank's gather fails at
+    once and its communicator is marked broken (a second gather is refused, exit 7).  A peer that
+    waits on the failed rank (the root on a sender that never sent; either rank in the length
+    all-gather) fails when its wait runs out, broken as well.  A sender whose blob was delivered
+    before the root's receive failed completes (exit 0): the run still fails, on the root, and the
+    bench's error flag is reduced over the ranks (bench.py program_sharded)."""
     res = _ranks("fail", 2, ZKL_NCCL_STUB_FAIL=op, ZKL_NCCL_STUB_FAIL_RANK=str(rank), ZKL_NCCL_STUB_TIMEOUT_S="5")
-    for rc, so, se in res:
-        assert rc == 7, (rc, so, se[-2000:])
+    assert tuple(rc for rc, _, _ in res) == want, [(rc, so, se[-1500:]) for rc, so, se in res]
     msgs = [json.loads(so.strip().splitlines()[-1]) for _, so, _ in res]
-    assert any("injected" in m["first"] for m in msgs)
+    assert "injected" in (msgs[rank]["first"] or "")
