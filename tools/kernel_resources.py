@@ -22,7 +22,10 @@ def kernel_resources(lib):
     out = {}
     with tempfile.TemporaryDirectory() as td:
         fb = os.path.join(td, "fb.bin")
-        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", lib], check=True, capture_output=True)
+        # an explicit output file: without one objcopy rewrites `lib` in place (which also breaks a
+        # process that has it mapped)
+        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", lib, os.path.join(td, "discard.so")],
+                       check=True, capture_output=True)
         data = open(fb, "rb").read()
         starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)]
         for k, a in enumerate(starts):

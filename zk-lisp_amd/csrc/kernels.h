@@ -44,6 +44,11 @@ struct HasherMont {
   uint32_t dom130[2][5];
   uint32_t r2_130[5];  // R'^2 mod p
   uint32_t dfe130[4][5];
+  // the 48-lane permutation (poseidon.hip pw_permute): MDS entries weighted by limb position,
+  // mdsl[i][k][u] = limbs of M[i][k] * 2^(26u) mod p (plain, canonical), and the round
+  // constants in R' form
+  uint32_t mdsl[12][12][5][5];
+  uint32_t rc130[27][12][5];
 };
 HasherMont make_hasher_mont(const HasherConsts& h);
 void upload_hasher_mont(const HasherMont& m, hipStream_t s);

@@ -85,6 +85,12 @@ HasherMont make_hasher_mont(const HasherConsts& h) {
   mont130(h.dom_merge, m.dfe130[DOM_MERGE]);
   mont130(h.dom_many, m.dfe130[DOM_MANY]);
   mont130(h.dom_int, m.dfe130[DOM_INT]);
+  fe w = fe_one();  // 2^(26u)
+  for (int u = 0; u < 5; u++, w = fe_mul(w, fe{1ull << 26, 0}))
+    for (int i = 0; i < 12; i++)
+      for (int k = 0; k < 12; k++) limbs26(fe_mul(h.mds[i * 12 + k], w), m.mdsl[i][k][u]);
+  for (int r = 0; r < 27; r++)
+    for (int i = 0; i < 12; i++) mont130(h.rc[r * 12 + i], m.rc130[r][i]);
   return m;
 }
 
@@ -205,14 +211,21 @@ __device__ __forceinline__ fe pg_bcast(const PGroup& P, fe v, int src) {
 // ---- wide lane groups (latency-bound levels) ------------------------------------------
 // PW_SPLIT (2 or 4) lanes per state element: lane SPLIT*e + h owns element e (every lane of
 // the element holds it) and the MDS row-e constants of columns COLS*h .. COLS*h + COLS-1
-// (COLS = 12 / SPLIT).  Each lane sums its COLS products and reduces them (REDC is linear:
-// REDC(a) + REDC(b) == (a + b) R^-1 mod p, and each output is < p + 2^109 since R = 2^156
-// >> p, so the sum of four plus a round constant keeps limbs < 2^28.4, inside the bounds
-// mont_cube and redc assume); the lanes of an element add their reduced parts with DPP
-// quad permutes instead of a second LDS exchange.  One state per wave at SPLIT 4 (lanes
-// 48..63 idle), two at SPLIT 2.  Used where a level has too few states to fill the SIMDs
-// (upper Merkle levels, small FRI layers, the FRI transcript): one permutation's dependency
-// chain bounds those levels.
+// (COLS = 12 / SPLIT).  Used where a level has too few states to fill the SIMDs (upper Merkle
+// levels, small FRI layers, the transcript kernels): one permutation's dependency chain bounds
+// those levels, so the round is built for a short chain rather than few
+// instructions per state.
+//
+// Radix R' = 2^130, as the matrix-core form: a state element is held as s R' (five 26-bit
+// limbs, lazily reduced), the cube is mont_cube130 (two five-digit REDCs) and gives s^3 R'.
+// The MDS layer needs no REDC at all: the cube y (limbs y_u) enters row e as
+// sum_u y_u (M[e][k] 2^(26u) mod p) with the limb-weighted constants c_hm.mdsl (linear, so the
+// R' factor passes through), i.e. 5 x 5 products per column into five 64-bit limb columns,
+// which one carry pass and a fold of the bits >= 128 (2^128 == 45 2^40 - 1) bring back to
+// five limbs of a value < 2^128 + 2^82.  The SPLIT lanes of an element add those parts with
+// DPP quad permutes, plus the round constant: limbs < 2^28.4, value < 2^130.4, inside what
+// mont_cube130 takes.  Against the R = 2^156 round this drops one REDC digit step from each of
+// the cube's two reductions and the whole six-step REDC of the MDS sum.
 #ifndef PW_SPLIT
 #define PW_SPLIT 4
 #endif
@@ -224,8 +237,8 @@ constexpr int PW_GROUP_WORDS = 60;  // cubes [l][12]
 constexpr int PW_WAVE_WORDS = (PW_PER_WAVE + 1) * PW_GROUP_WORDS;  // + the idle partial group
 
 struct PWGroup {
-  uint32_t m[PW_COLS][5];  // MDS row e, columns COLS*h .. (Montgomery)
-  uint32_t* x;             // cubes: x[limb * 12 + e]
+  uint32_t c[PW_COLS][5][5];  // c[k][u][l] = limb l of M[e][COLS*h + k] * 2^(26u) mod p
+  uint32_t* x;                // cubes: x[limb * 12 + e]
   int e, h, g;
 };
 
@@ -250,25 +263,53 @@ __device__ __forceinline__ void pw_init(PWGroup& P, uint32_t* lds) {
 #pragma unroll
   for (int k = 0; k < PW_COLS; k++)
 #pragma unroll
-    for (int l = 0; l < 5; l++) P.m[k][l] = c_hm.mds[P.e][PW_COLS * P.h + k][l];
+    for (int u = 0; u < 5; u++)
+#pragma unroll
+      for (int l = 0; l < 5; l++) P.c[k][u][l] = c_hm.mdsl[P.e][PW_COLS * P.h + k][u][l];
 }
 
-// sum of v over the SPLIT lanes of this lane's element (DPP quad_perm [1,0,3,2], [2,3,0,1])
+// sum of v over the SPLIT lanes of this lane's element (DPP quad_perm [1,0,3,2], [2,3,0,1]);
+// the permuted operand's old value is 0, so each step can issue as one v_add_u32_dpp
 __device__ __forceinline__ uint32_t pw_elem_sum(uint32_t v) {
-  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
-  if (PW_SPLIT == 4) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+  if (PW_SPLIT == 4) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
   return v;
 }
 
+// five 64-bit limb columns (each < 2^60) -> five limbs of a congruent value < 2^128 + 2^82:
+// limbs 0, 1, 3 < 2^26, limb 2 < 2^26 + 8, limb 4 < 2^24.  The bits >= 128 of column 4 fold
+// as t 2^128 == t (737279 2^26 + 2^26 - 1) for its low word's top byte t and as
+// hi 2^136 == hi (188743680 2^26 - 2^8) for its high word hi (< 2^28).
+__device__ __forceinline__ void pw_fold(uint64_t col[5], uint32_t x[5]) {
+  uint32_t l[4];
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    col[t + 1] += col[t] >> 26;
+    l[t] = (uint32_t)col[t] & M26;
+  }
+  const uint32_t lo4 = (uint32_t)col[4], hi4 = (uint32_t)(col[4] >> 32);
+  const uint32_t t = lo4 >> 24;
+  // a >= -2^36; b >= 188743680 whenever hi4 > 0, so b + (a >> 26) >= 0
+  const int64_t a = (int64_t)((uint64_t)t * M26 + l[0]) - (int64_t)((uint64_t)hi4 << 8);
+  const uint64_t b = (uint64_t)t * 737279u + (uint64_t)hi4 * 188743680u + l[1];
+  const uint64_t bb = b + (uint64_t)(a >> 26);
+  x[0] = (uint32_t)a & M26;
+  x[1] = (uint32_t)bb & M26;
+  const uint32_t x2 = l[2] + (uint32_t)(bb >> 26);
+  x[2] = x2 & M26;
+  x[3] = l[3] + (x2 >> 26);
+  x[4] = lo4 & 0xFFFFFFu;
+}
+
 __device__ __forceinline__ void pw_permute(PWGroup& P, uint32_t s[5]) {
-  const uint32_t* rcp = &c_hm.rc[0][P.e][0];
+  const uint32_t* rcp = &c_hm.rc130[0][P.e][0];
 #pragma unroll 1
   for (int r = 0; r < 27; r++, rcp += 60) {
     uint32_t rc[5];
 #pragma unroll
     for (int l = 0; l < 5; l++) rc[l] = rcp[l];
     uint32_t t[5];
-    mont_cube(s, t);
+    mont_cube130(s, t);
     if (P.h == 0) {
 #pragma unroll
       for (int l = 0; l < 5; l++) P.x[l * 12 + P.e] = t[l];
@@ -280,11 +321,15 @@ __device__ __forceinline__ void pw_permute(PWGroup& P, uint32_t s[5]) {
 #pragma unroll
       for (int k = 0; k < PW_COLS; k++) tk[k][l] = P.x[l * 12 + PW_COLS * P.h + k];
     __builtin_amdgcn_wave_barrier();
-    uint64_t col[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t col[5] = {0, 0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < PW_COLS; k++) mac5(tk[k], P.m[k], col);
+    for (int k = 0; k < PW_COLS; k++)
+#pragma unroll
+      for (int u = 0; u < 5; u++)
+#pragma unroll
+        for (int l = 0; l < 5; l++) col[l] += (uint64_t)tk[k][u] * P.c[k][u][l];
     uint32_t part[5];
-    redc(col, part);
+    pw_fold(col, part);
 #pragma unroll
     for (int l = 0; l < 5; l++) s[l] = pw_elem_sum(part[l]) + rc[l];
   }
@@ -295,19 +340,19 @@ __device__ __forceinline__ fe pw_sponge(PWGroup& P, bool live, int nmsg, Loader 
   uint32_t s[5];
 #pragma unroll
   for (int l = 0; l < 5; l++)
-    s[l] = P.e == 0 ? c_hm.dfe[D][l] : P.e == 10 ? c_hm.dom[0][l] : P.e == 11 ? c_hm.dom[1][l] : 0u;
+    s[l] = P.e == 0 ? c_hm.dfe130[D][l] : P.e == 10 ? c_hm.dom130[0][l] : P.e == 11 ? c_hm.dom130[1][l] : 0u;
   const int T = nmsg + 1;
   for (int b = 0; b * 10 < T; b++) {
     const int idx = b * 10 + P.e;
     if (live && P.e < 10 && idx >= 1 && idx < T) {
       uint32_t m[5];
-      to_mont(ld(idx - 1), m);
+      to_mont130(ld(idx - 1), m);
 #pragma unroll
       for (int l = 0; l < 5; l++) s[l] += m[l];
     }
     pw_permute(P, s);
   }
-  return from_mont(s);  // state element 0 in lanes with e == 0
+  return from_mont130(s);  // state element 0 in lanes with e == 0
 }
 
 __device__ __forceinline__ fe pw_bcast(const PWGroup& P, fe v, int src_e) {
@@ -457,14 +502,6 @@ void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np
     hash_rows_kernel<1><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, merge, d_out, split);
   else
     hash_rows_kernel<0><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, merge, d_out, split);
-}
-
-__global__ __launch_bounds__(256) void merkle_level_wide_kernel(fe* nodes, size_t lvl) {
-  PW_SETUP();
-  const bool live = P.g < PW_PER_WAVE && item < lvl;
-  const size_t i = lvl + (live ? item : 0);
-  fe d = pw_sponge<DOM_MERGE>(P, live, 2, [&](int j) { return nodes[2 * i + j]; });
-  if (live && P.e == 0 && P.h == 0) nodes[i] = d;
 }
 
 // Tree top: several levels per launch.  Workgroup g (4 waves, 8 wide groups, one wave per
