@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <memory>
+#include <stdexcept>
 #include <vector>
 
 #include "field.h"
@@ -62,57 +63,56 @@ struct Plan {
   std::vector<uint64_t> node;  // the lists back to back
   std::vector<uint32_t> len;   // entries per list
 };
-inline Plan batch_plan(size_t n_leaves, const std::vector<size_t>& idx) {
+// plan of idx[0..Q) into P (its vectors keep their capacity across calls: no allocation in the
+// steady state).  Q <= 256 (ProofOptions' num_queries is a byte).
+inline void batch_plan_into(size_t n_leaves, const size_t* idx, size_t Q, Plan& P) {
+  if (Q > 256) throw std::invalid_argument("batch_plan: more than 256 query positions");
   const int depth = ilog2(n_leaves);
-  const size_t Q = idx.size();
-  // scratch kept per thread (one plan per tree and FRI layer of every proof: no allocation in
-  // the steady state)
-  static thread_local std::vector<size_t> sbuf, scur;
-  static thread_local std::vector<uint64_t> stmp;
-  static thread_local std::vector<uint32_t> scnt;
   // normalised leaf pairs (sorted, unique) and the requested leaves (sorted)
-  sbuf.resize(2 * Q + 2);
-  size_t* norm = sbuf.data();
-  size_t* req = norm + Q + 1;
+  size_t norm[256], req[256], cur[256], nxt[256];
+  uint32_t cnt[256];
   for (size_t k = 0; k < Q; k++) { norm[k] = idx[k] & ~(size_t)1; req[k] = idx[k]; }
   std::sort(norm, norm + Q);
   const size_t L = (size_t)(std::unique(norm, norm + Q) - norm);
   std::sort(req, req + Q);
   // list k takes at most two leaves and one node per level: fixed-stride scratch, compacted
   const size_t stride = (size_t)depth + 2;
-  stmp.resize(L * stride);
-  scnt.assign(L, 0);
-  scur.resize(2 * L + 2);
-  uint64_t* tmp = stmp.data();
-  uint32_t* cnt = scnt.data();
-  size_t *cur = scur.data(), *nxt = cur + L + 1;
+  P.node.resize(L * stride);
+  uint64_t* tmp = P.node.data();
+  size_t r = 0;  // req and norm are both ascending: one merge pass finds the requested leaves
   for (size_t k = 0; k < L; k++) {
-    for (size_t j = norm[k]; j < norm[k] + 2; j++)
-      if (!std::binary_search(req, req + Q, j)) tmp[k * stride + cnt[k]++] = n_leaves + j;
+    cnt[k] = 0;
+    for (size_t j = norm[k]; j < norm[k] + 2; j++) {
+      while (r < Q && req[r] < j) r++;
+      if (!(r < Q && req[r] == j)) tmp[k * stride + cnt[k]++] = n_leaves + j;
+    }
     cur[k] = (norm[k] + n_leaves) >> 1;
   }
   size_t nc = L;
+  size_t *a = cur, *b = nxt;
   for (int lvl = 1; lvl < depth; lvl++) {
     size_t nn = 0;
     for (size_t i = 0; i < nc; i++) {
-      const size_t sib = cur[i] ^ 1;
-      if (i + 1 < nc && cur[i + 1] == sib) i++;
+      const size_t sib = a[i] ^ 1;
+      if (i + 1 < nc && a[i + 1] == sib) i++;
       else tmp[i * stride + cnt[i]++] = sib;
-      nxt[nn++] = sib >> 1;
+      b[nn++] = sib >> 1;
     }
-    std::swap(cur, nxt);
+    std::swap(a, b);
     nc = nn;
   }
-  Plan P;
+  // compact the lists in place (list k starts at or after where it is moved to)
   P.len.assign(cnt, cnt + L);
-  size_t tot = 0;
-  for (size_t k = 0; k < L; k++) tot += cnt[k];
-  P.node.resize(tot);
   size_t o = 0;
   for (size_t k = 0; k < L; k++) {
-    memcpy(P.node.data() + o, tmp + k * stride, cnt[k] * sizeof(uint64_t));
+    memmove(tmp + o, tmp + k * stride, cnt[k] * sizeof(uint64_t));
     o += cnt[k];
   }
+  P.node.resize(o);
+}
+inline Plan batch_plan(size_t n_leaves, const std::vector<size_t>& idx) {
+  Plan P;
+  batch_plan_into(n_leaves, idx.data(), idx.size(), P);
   return P;
 }
 

@@ -131,8 +131,10 @@ struct zkl_ctx {
   int kfam_n[ZKL_NUM_KFAMILIES] = {0};
   // host scratch kept across proofs (gather plan, proof bytes, the AIR instance with its ~2.9e5
   // assertions): no per-proof allocation of the large host buffers
-  std::vector<uint64_t> addrs_s;
   std::vector<uint8_t> proof_s;
+  Plan tplan_s;                              // trace / constraint tree query plan
+  std::vector<Plan> fplan_s;                 // FRI layer plans
+  std::vector<std::vector<size_t>> fpos_s;   // FRI layer query positions
   AirInstance air;
   // zkl_hip_trace_buffer: pinned host traces the caller fills in place (two slots: one filled
   // while the other's proof runs); zkl_hip_prove_segment DMAs columns straight from them
@@ -900,41 +902,55 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   const size_t nq = pos.size();
 
   HT("q_sorted");
-  // gather plan: trace rows, comp rows, trace/comp tree nodes, FRI values + tree nodes
-  std::vector<uint64_t>& addrs = C->addrs_s;
-  addrs.clear();
-  addrs.reserve(nq * ((size_t)W + Cc) + 2 * nq * (size_t)(logN + 2) * (nl + 2) + 64);
-  auto A = [&](const fe* p) { addrs.push_back((uint64_t)(uintptr_t)p); };
+  // gather plan: trace rows, comp rows, trace/comp tree nodes, FRI values + tree nodes.  Host
+  // work between two device round trips (the GPU idles through it): written into per-context
+  // scratch that keeps its capacity, no allocation in the steady state.
+  // upper bound of the address count: rows, two tree plans, per FRI layer two values and a plan
+  // per position (a plan has at most depth + 2 entries per position)
+  const size_t na_max = nq * ((size_t)W + Cc) + 2 * nq * ((size_t)logN + 2) + (size_t)nl * nq * ((size_t)logN + 4);
+  C->h_addr.ensure(na_max * 8);
+  uint64_t* const abase = C->h_addr.at<uint64_t>();
+  uint64_t* ap = abase;
+  for (size_t k = 0; k < nq; k++) {
+    const fe* rp = C->lde.f() + lde_pos(pos[k], N, split);
+    for (uint32_t c = 0; c < W; c++) *ap++ = (uint64_t)(uintptr_t)(rp + (size_t)c * N);
+  }
   for (size_t k = 0; k < nq; k++)
-    for (uint32_t c = 0; c < W; c++) A(C->lde.f() + (size_t)c * N + lde_pos(pos[k], N, split));
-  for (size_t k = 0; k < nq; k++) for (int j = 0; j < Cc; j++) A(C->clde.f() + (size_t)j * N + pos[k]);
-  auto tplan = batch_plan(N, pos);
-  for (auto ix : tplan.node) A(C->tree.f() + ix);
-  for (auto ix : tplan.node) A(C->ctree.f() + ix);
-  std::vector<std::vector<size_t>> fpos(nl);
-  std::vector<Plan> fplan(nl);
+    for (int j = 0; j < Cc; j++) *ap++ = (uint64_t)(uintptr_t)(C->clde.f() + (size_t)j * N + pos[k]);
+  auto append_nodes = [&](const fe* tree, const Plan& plan) {
+    for (uint64_t ix : plan.node) *ap++ = (uint64_t)(uintptr_t)(tree + ix);
+  };
+  Plan& tplan = C->tplan_s;
+  batch_plan_into(N, pos.data(), nq, tplan);
+  append_nodes(C->tree.f(), tplan);
+  append_nodes(C->ctree.f(), tplan);
+  std::vector<std::vector<size_t>>& fpos = C->fpos_s;
+  std::vector<Plan>& fplan = C->fplan_s;
+  if (fpos.size() < (size_t)nl) fpos.resize(nl);
+  if (fplan.size() < (size_t)nl) fplan.resize(nl);
   {
-    std::vector<size_t> p = pos;
     size_t dsz = N;
     for (int d = 0; d < nl; d++) {
-      size_t h = dsz / 2;
-      std::vector<size_t> f;
-      for (size_t x : p) { size_t y = x % h; if (std::find(f.begin(), f.end(), y) == f.end()) f.push_back(y); }
-      fpos[d] = f;
-      for (size_t y : f) { A(layer_ev(d) + y); A(layer_ev(d) + y + h); }
-      fplan[d] = batch_plan(h, f);
-      for (auto ix : fplan[d].node) A(C->fri_tree.f() + tr_off[d] + ix);
-      p = f;
+      const size_t h = dsz / 2;
+      const std::vector<size_t>& p = d ? fpos[d - 1] : pos;
+      std::vector<size_t>& f = fpos[d];
+      f.clear();
+      for (size_t x : p) {  // fold positions, first occurrence kept (FriProver::build_proof order)
+        const size_t y = x & (h - 1);
+        if (std::find(f.begin(), f.end(), y) == f.end()) f.push_back(y);
+      }
+      for (size_t y : f) { *ap++ = (uint64_t)(uintptr_t)(layer_ev(d) + y); *ap++ = (uint64_t)(uintptr_t)(layer_ev(d) + y + h); }
+      batch_plan_into(h, f.data(), f.size(), fplan[d]);
+      append_nodes(C->fri_tree.f() + tr_off[d], fplan[d]);
       dsz = h;
     }
   }
+  if ((size_t)(ap - abase) > na_max) throw std::runtime_error("internal: gather plan bound");
   HT("q_planned");
-  const size_t na_g = addrs.size();
+  const size_t na_g = (size_t)(ap - abase);
   C->gaddr.ensure((na_g + na_g / 4) * 8);
   C->gout.ensure((na_g + na_g / 4) * sizeof(fe));
-  C->h_addr.ensure(na_g * 8);
   C->h_gv.ensure(na_g * sizeof(fe));
-  memcpy(C->h_addr.p, addrs.data(), na_g * 8);
   HIPCHECK(hipMemcpyAsync(C->gaddr.p, C->h_addr.p, na_g * 8, hipMemcpyHostToDevice, s));
   launch_gather((const uint64_t*)C->gaddr.p, na_g, C->gout.f(), s);
   check_launch("query gather");
@@ -963,24 +979,38 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     cm.digest(rem_commit);
     P.vec(cm);
   }
-  auto emit_multiproof = [&](Bytes& b, const Plan& plan, int depth) {
-    b.u8((uint8_t)depth);
-    b.u8((uint8_t)plan.len.size());
+  // BatchMerkleProof bytes of a plan whose node values start at gv[g]: [depth][lists] then per
+  // list [len][len digests]; written with its vint length prefix (Vec<u8> of the proof)
+  auto mp_len = [](const Plan& plan) {
+    size_t n = 2 + plan.len.size();
+    for (uint32_t l : plan.len) n += 32 * (size_t)l;
+    return n;
+  };
+  auto emit_multiproof = [&](const Plan& plan, int depth, size_t g) {
+    const size_t len = mp_len(plan);
+    P.usize(len);
+    const size_t o = P.v.size();
+    P.v.resize(o + len);
+    uint8_t* w = P.v.data() + o;
+    *w++ = (uint8_t)depth;
+    *w++ = (uint8_t)plan.len.size();
     for (uint32_t l : plan.len) {
-      b.u8((uint8_t)l);
-      for (uint32_t k = 0; k < l; k++) b.digest(gv[gi++]);
+      *w++ = (uint8_t)l;
+      for (uint32_t k = 0; k < l; k++, w += 32) {  // digest: the 16 value bytes + 16 zero bytes
+        memcpy(w, gv + g++, 16);
+        memset(w + 16, 0, 16);
+      }
     }
   };
-  Bytes tv, cv, tp, cpb;
-  tv.raw(gv + gi, nq * W * sizeof(fe));  // felem = the 16 LE bytes of the canonical value
-  gi += nq * W;
-  cv.raw(gv + gi, nq * Cc * sizeof(fe));
-  gi += nq * Cc;
-  emit_multiproof(tp, tplan, logN);
-  emit_multiproof(cpb, tplan, logN);
+  const size_t g_rows = 0, g_crows = nq * W, g_tnodes = nq * ((size_t)W + Cc), g_cnodes = g_tnodes + tplan.node.size();
   P.usize(1);
-  P.vec(tv); P.vec(tp);
-  P.vec(cv); P.vec(cpb);
+  P.usize(nq * W * sizeof(fe));  // felem = the 16 LE bytes of the canonical value
+  P.raw(gv + g_rows, nq * W * sizeof(fe));
+  emit_multiproof(tplan, logN, g_tnodes);
+  P.usize(nq * Cc * sizeof(fe));
+  P.raw(gv + g_crows, nq * Cc * sizeof(fe));
+  emit_multiproof(tplan, logN, g_cnodes);
+  gi = g_cnodes + tplan.node.size();
   {
     Bytes ts, es;
     for (auto& v : tz) ts.felem(v);
@@ -991,10 +1021,12 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   }
   P.usize((uint64_t)nl);
   for (int d = 0; d < nl; d++) {
-    Bytes lv, lp;
-    for (size_t k = 0; k < fpos[d].size(); k++) { lv.felem(gv[gi++]); lv.felem(gv[gi++]); }
-    emit_multiproof(lp, fplan[d], ilog2((N >> d) / 2));
-    P.vec(lv); P.vec(lp);
+    const size_t nv = 2 * fpos[d].size();
+    P.usize(nv * sizeof(fe));
+    P.raw(gv + gi, nv * sizeof(fe));
+    gi += nv;
+    emit_multiproof(fplan[d], ilog2((N >> d) / 2), gi);
+    gi += fplan[d].node.size();
   }
   {
     Bytes rv;
