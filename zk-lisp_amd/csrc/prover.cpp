@@ -99,6 +99,7 @@ struct zkl_ctx {
   DBuf roots, iroots, mroots, miroots, opow, opow_n, pertab;
   // work buffers
   DBuf trace, coef, lde, parts, tree, ce, bvec, bm, clde, ctree, deep, draws, pw, oodv, oodf, txs, asl, ast, asv, ars;
+  DBuf lcoef;  // coefficients (scaled, in LDE input order) of the boundary and composition column LDEs
   DBuf fri_ev, fri_tree, best, gaddr, gout, flag;
   DBuf xinv;    // batch-inverted coset denominators of DEEP (z-dependent)
   DBuf posep;   // PoseidonAir block's share of the transition sum per CE point (Poseidon layouts)
@@ -609,8 +610,11 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   {
     KScope k(C, KF_NTT);
     launch_ntt_stages(C->bvec.f(), nb + 1, n, true, 0, logn - 1, mroots, Ntab, s);  // forward, bit-reversed out
-    launch_broadcast(C->bvec.f(), n, 1, 0, nb + 1, n, ce, C->opow.f(), fe_one(), true, C->bm.f(), s);
-    launch_ntt_stages(C->bm.f(), nb + 1, ce, false, ilog2(ce / n), logce - 1, mroots, Ntab, s);
+    // reversed, scaled coefficients, then the DIT over the CE coset whose first pass reads each
+    // of them blowup times (the copies are not materialised; same values as a broadcast)
+    C->lcoef.ensure((size_t)std::max<uint32_t>(nb + 1, Cc) * n * sizeof(fe));
+    launch_broadcast(C->bvec.f(), n, 1, 0, nb + 1, n, n, C->opow.f(), fe_one(), true, C->lcoef.f(), s);
+    launch_lde_from_coeffs(C->lcoef.f(), nb + 1, n, ce, mroots, Ntab, C->bm.f(), s, false);
   }
   check_launch("boundary tables");
 
@@ -669,10 +673,10 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     for (int j = 0; j < Cc; j++) {
       // column j coefficient k' = chat[j n + k'] * 3^(-(j n + k')) / ce; LDE multiplies by 3^k'
       fe mult = fe_mul(fe_pow64(inv3, (uint64_t)j * n), inv_ce);
-      launch_broadcast(C->ce.f(), 0, ce / n, bitrev_u((uint32_t)j, loge), 1, n, N, nullptr, mult, false,
-                       C->clde.f() + (size_t)j * N, s);
+      launch_broadcast(C->ce.f(), 0, ce / n, bitrev_u((uint32_t)j, loge), 1, n, n, nullptr, mult, false,
+                       C->lcoef.f() + (size_t)j * n, s);
     }
-    launch_ntt_stages(C->clde.f(), Cc, N, false, ilog2(B), logN - 1, mroots, Ntab, s);
+    launch_lde_from_coeffs(C->lcoef.f(), Cc, n, N, mroots, Ntab, C->clde.f(), s, false);
   }
   check_launch("composition polynomial LDE");
   C->ctree.ensure(2 * N * sizeof(fe));
@@ -955,6 +959,10 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   launch_gather((const uint64_t*)C->gaddr.p, na_g, C->gout.f(), s);
   check_launch("query gather");
   HIPCHECK(hipMemcpyAsync(C->h_gv.p, C->gout.p, na_g * sizeof(fe), hipMemcpyDeviceToHost, s));
+  // the proof's device work ends here: its closing stage events go in before the wait, so
+  // T.finish() finds them complete instead of queueing a record behind it and waiting again
+  T.mark(9);
+  T.mark(10);
   HIPCHECK(hipStreamSynchronize(s));
   HT("q_gathered");
   const fe* gv = C->h_gv.at<fe>();
@@ -1037,8 +1045,6 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   P.u64(nonce);
   if (gi != na_g) throw std::runtime_error("internal: gather plan mismatch");
   HT("serialised");
-  T.mark(9);
-  T.mark(10);
   T.finish();
   HT("stage_events");
   resolve_kernel_times(C);
