@@ -131,6 +131,10 @@ void launch_ntt_stages(fe* d_data, size_t n_cols, size_t N, bool dif, int lo_log
 // d_coef.
 // want_split: store the evaluations in the split layout (lde_pos below) when the last pass
 // supports it; returns 1 when the output is split, 0 when it is in natural order.
+// all stages of a DIF iNTT of n-element columns (natural in, bit-reversed out), reading src
+// (nullptr: in place in d) and storing element i of each column times scale[bitrev(i)]
+void launch_intt_scaled(const fe* d_src, fe* d_data, size_t n_cols, size_t n, MontTab iroots, size_t Ntab,
+                        const fe* d_scale, hipStream_t s);
 int launch_lde_from_coeffs(const fe* d_coef, size_t n_cols, size_t n, size_t N, MontTab roots, size_t Ntab, fe* d_out,
                            hipStream_t s, bool want_split = false);
 // Even/odd split layout of a trace LDE column.  Write the N = 256 S rows as

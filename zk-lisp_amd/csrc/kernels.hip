@@ -106,13 +106,15 @@ void build_mont_table(const fe* w, size_t N, void* d_buf, hipStream_t s) {
   ZKL_HIPCHECK(hipStreamSynchronize(s));
 }
 
-// src != nullptr (first DIT pass of an LDE): element i of column c is read from
-// src[c * (N >> src_logb) + (i >> src_logb)] instead of data, i.e. the blowup copies of the
-// (scaled, bit-reversed) coefficients are generated on load rather than materialised.
+// src != nullptr (first DIT pass of an LDE, first DIF pass of an out-of-place iNTT): element i
+// of column c is read from src[c * (N >> src_logb) + (i >> src_logb)] instead of data, i.e. the
+// blowup copies of the (scaled, bit-reversed) coefficients are generated on load rather than
+// materialised.  scale != nullptr (last DIF pass): element i of a column is stored multiplied by
+// scale[bitrev(i)] (the coefficient scaling of an iNTT whose output is bit-reversed).
 template <bool DIF>
 __global__ __launch_bounds__(NTT_THREADS) void ntt_pass_kernel(fe* __restrict__ data, size_t ncols, int logN, int r,
                                                        int logS, MontTab roots, int logTab, const fe* __restrict__ src,
-                                                       int src_logb) {
+                                                       int src_logb, const fe* __restrict__ scale = nullptr) {
   __shared__ fe buf[NTT_ELEMS + NTT_ELEMS / 16];
   const int R = 1 << r;
   const int G = NTT_ELEMS >> r;
@@ -201,7 +203,7 @@ __global__ __launch_bounds__(NTT_THREADS) void ntt_pass_kernel(fe* __restrict__ 
     int t = gfast ? (e / G) : (e & (R - 1));
     bool ok;
     size_t a = addr(g, t, ok);
-    if (ok) data[a] = buf[g * pitch + t];
+    if (ok) data[a] = scale ? fe_mul(buf[g * pitch + t], scale[bitrev((uint32_t)(a & Nmask), logN)]) : buf[g * pitch + t];
   }
 }
 
@@ -581,8 +583,9 @@ static bool dit_split_ok(size_t N, int lo, int hi) {
   return rs.back() == 8 && ((size_t)1 << cur) >= (size_t)NTT8_G && (N >> 8) >= (size_t)NTT8_G;
 }
 
+// DIF: src (out of place) feeds the first pass, scale the last pass's stores (see ntt_pass_kernel)
 static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, MontTab roots, size_t Ntab,
-                       const fe* src, int src_logb, hipStream_t s, int split = 0) {
+                       const fe* src, int src_logb, hipStream_t s, int split = 0, const fe* scale = nullptr) {
   int logN = ilog2s(N), logTab = ilog2s(Ntab);
   if (hi < lo) return;
   const std::vector<int> rs = ntt_split(hi - lo + 1);
@@ -593,8 +596,8 @@ static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
       int logS = cur - r + 1;
       size_t groups = (N >> r) * ncols;
       size_t G = NTT_ELEMS >> r;
-      ntt_pass_kernel<true><<<(unsigned)((groups + G - 1) / G), NTT_THREADS, 0, s>>>(d, ncols, logN, r, logS, roots, logTab,
-                                                                             nullptr, 0);
+      ntt_pass_kernel<true><<<(unsigned)((groups + G - 1) / G), NTT_THREADS, 0, s>>>(
+          d, ncols, logN, r, logS, roots, logTab, k + 1 == rs.size() ? src : nullptr, 0, k == 0 ? scale : nullptr);
       cur -= r;
     }
   } else {
@@ -632,6 +635,13 @@ static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
 void launch_ntt_stages(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, MontTab roots, size_t Ntab,
                        hipStream_t s) {
   ntt_passes(d, ncols, N, dif, lo, hi, roots, Ntab, nullptr, 0, s);
+}
+
+void launch_intt_scaled(const fe* src, fe* d, size_t ncols, size_t n, MontTab iroots, size_t Ntab, const fe* scale,
+                        hipStream_t s) {
+  const int logn = ilog2s(n);
+  if (logn == 0) throw std::invalid_argument("launch_intt_scaled: n must be at least 2");
+  ntt_passes(d, ncols, n, true, 0, logn - 1, iroots, Ntab, src, 0, s, 0, scale);
 }
 
 int launch_lde_from_coeffs(const fe* d_coef, size_t ncols, size_t n, size_t N, MontTab roots, size_t Ntab, fe* d_out,

@@ -469,10 +469,10 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   // columns [c0, c0 + nc): iNTT -> n*coef bit-reversed, scale c_k * 3^k (coset shift), DIT
   // every chunk takes the same pass split, so all columns share one layout
   int split = -1;
-  auto lde_cols = [&](uint32_t c0, uint32_t nc) {
+  // src: the caller's resident trace, read by the iNTT's first pass (nullptr: already in coef)
+  auto lde_cols = [&](uint32_t c0, uint32_t nc, const fe* src) {
     fe* cf = C->coef.f() + (size_t)c0 * n;
-    launch_ntt_stages(cf, nc, n, true, 0, logn - 1, miroots, Ntab, s);
-    launch_scale_bitrev(cf, nc, n, C->opow_n.f(), s);
+    launch_intt_scaled(src, cf, nc, n, miroots, Ntab, C->opow_n.f(), s);
     const int sp = launch_lde_from_coeffs(cf, nc, n, N, mroots, Ntab, C->lde.f() + (size_t)c0 * N, s, g_lde_split);
     // the row hash, evaluator and DEEP read every column with one layout (the NTT mode cannot
     // change during a proof: zkl_hip_set_ntt_mode refuses while one is in flight)
@@ -481,12 +481,11 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   };
   if (trace_on_host) {
     KScope k(C, KF_NTT);
-    upload_trace_chunked(C, d_trace_in, W, n, s, lde_cols);
+    upload_trace_chunked(C, d_trace_in, W, n, s, [&](uint32_t c0, uint32_t nc) { lde_cols(c0, nc, nullptr); });
   } else {
     C->up_ms = 0;
-    HIPCHECK(hipMemcpyAsync(C->coef.p, d_trace_in, (size_t)W * n * sizeof(fe), hipMemcpyDeviceToDevice, s));
     KScope k(C, KF_NTT);
-    lde_cols(0, W);
+    lde_cols(0, W, (const fe*)d_trace_in);
   }
   check_launch("trace LDE");
   if (split < 0) split = 0;
