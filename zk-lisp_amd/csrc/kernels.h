@@ -89,7 +89,12 @@ void launch_deep_coeffs(const fe* d_gam, uint32_t W, uint32_t C, const fe* d_fra
 void launch_hash_rows(const fe* d_mat, uint32_t n_cols, size_t n_rows, uint32_t num_partitions,
                       uint32_t hash_rate, fe* d_tmp, fe* d_out, hipStream_t s, int tag = 0, int split = 0);
 // Merkle tree: d_nodes[n..2n) must hold the leaves; fills d_nodes[1..n).
-void launch_merkle(fe* d_nodes, size_t n_leaves, hipStream_t s);
+// coin_mode (d_coin, d_root_out): the transcript step after the tree runs in the launch that
+// reaches the root -- 1: coin[0] = merge(coin[0], root) (the trace / constraint root reseed), 2:
+// that and coin[1] = merge_with_int(coin[0], 1) (a FRI layer's alpha); the root is copied to
+// *d_root_out when that is not null
+void launch_merkle(fe* d_nodes, size_t n_leaves, hipStream_t s, fe* d_coin = nullptr, fe* d_root_out = nullptr,
+                   int coin_mode = 0);
 // out[i] = merge_with_int(seed, base + 1 + i)   (RandomCoin::draw, counter base+1+i)
 // d_seed != nullptr: the seed is read from device memory (the device-side transcript)
 void launch_draws(fe seed, uint64_t base, size_t k, fe* d_out, hipStream_t s, const fe* d_seed = nullptr);
@@ -98,7 +103,6 @@ void launch_grind(fe seed, uint64_t base, uint32_t count, uint32_t bits, unsigne
                   const fe* d_seed = nullptr);
 // Device-side transcript (DefaultRandomCoin with the seed in device memory):
 // coin[0] = merge(coin[0], *value) and *value_out = *value (nullable)
-void launch_coin_reseed(fe* d_coin, const fe* d_value, fe* d_value_out, hipStream_t s);
 // FRI remainder coefficients (rem[0..rlen), highest degree first), their hash_elements
 // commitment rem[rlen], and coin[0] = merge(coin[0], rem[rlen]); wk[k] = w^-k, sk[k] = 3^-k / Nr
 void launch_fri_remainder(const fe* d_ev, uint32_t Nr, uint32_t rlen, const fe* wk, const fe* sk, fe* d_coin,
@@ -233,12 +237,11 @@ void launch_deep(const fe* d_lde, const fe* d_clde, const fe* d_roots, size_t Nt
                  const DerivedConsts* dD, const fe* d_dinv /* from launch_deep_denoms */, fe* d_out, hipStream_t s,
                  int split = 0);
 void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s);
-// alpha read from device memory (written by launch_fri_coin)
+// alpha read from device memory (coin[1], written by the layer tree's launch_merkle)
 void launch_fri_fold(const fe* d_ev, size_t Nd, const fe* d_alpha, const fe* d_iroots, size_t Ntab, fe* d_out,
                      hipStream_t s);
 // device transcript step of one FRI layer: coin[0] = merge(coin[0], *root); coin[1] = alpha
 // = merge_with_int(coin[0], 1); *root_out = *root
-void launch_fri_coin(fe* d_coin, const fe* d_root, fe* d_root_out, hipStream_t s);
 // gather 16-byte elements from absolute device addresses
 void launch_gather(const uint64_t* d_addrs, size_t k, fe* d_out, hipStream_t s);
 

@@ -511,7 +511,12 @@ void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np
 // permutation-latency-bound levels.
 constexpr int TOP_WAVES = 8 / PW_PER_WAVE;
 constexpr int TOP_SLOTS = TOP_WAVES * PW_PER_WAVE;  // 8
-__global__ __launch_bounds__(64 * TOP_WAVES) void merkle_top_kernel(fe* nodes, size_t lvl, int cnt) {
+// coin_mode (the launch that reaches the root, one workgroup): after the root, wave 0 runs the
+// transcript step that follows the tree -- 1: coin[0] = merge(coin[0], root) (the trace and
+// constraint roots), 2: that and coin[1] = merge_with_int(coin[0], 1) (a FRI layer: alpha) --
+// and copies the root to *root_out, instead of a launch of its own.
+__global__ __launch_bounds__(64 * TOP_WAVES) void merkle_top_kernel(fe* nodes, size_t lvl, int cnt, fe* coin,
+                                                                    fe* root_out, int coin_mode) {
   __shared__ __align__(16) uint32_t pw_lds[TOP_WAVES * PW_WAVE_WORDS];
   PWGroup P;
   pw_init(P, pw_lds);
@@ -527,13 +532,30 @@ __global__ __launch_bounds__(64 * TOP_WAVES) void merkle_top_kernel(fe* nodes, s
     }
     __syncthreads();
   }
+  if (coin_mode && threadIdx.x < 64) {  // wave 0 of the single workgroup
+    const bool live = P.g == 0;
+    const fe seed = coin[0], r = nodes[1];
+    fe s1 = pw_sponge<DOM_MERGE>(P, live, 2, [&](int j) { return j == 0 ? seed : r; });
+    fe a = fe_zero();
+    if (coin_mode == 2) {
+      s1 = pw_bcast(P, s1, 0);
+      a = pw_sponge<DOM_INT>(P, live, 2, [&](int j) { return j == 0 ? s1 : fe{1, 0}; });
+    }
+    if (threadIdx.x == 0) {
+      coin[0] = s1;
+      if (coin_mode == 2) coin[1] = a;
+      if (root_out) *root_out = r;
+    }
+  }
 }
 
-void launch_merkle(fe* d_nodes, size_t n, hipStream_t s) {
+void launch_merkle(fe* d_nodes, size_t n, hipStream_t s, fe* d_coin, fe* d_root_out, int coin_mode) {
   for (size_t lvl = n / 2; lvl >= 1;) {
     if (lvl <= PW_MAX_ITEMS) {
       const size_t cnt = std::min<size_t>(lvl, TOP_SLOTS);
-      merkle_top_kernel<<<(unsigned)(lvl / cnt), 64 * TOP_WAVES, 0, s>>>(d_nodes, lvl, (int)cnt);
+      const bool last = lvl / (cnt * 2) == 0;  // this launch reaches the root
+      merkle_top_kernel<<<(unsigned)(lvl / cnt), 64 * TOP_WAVES, 0, s>>>(d_nodes, lvl, (int)cnt, d_coin, d_root_out,
+                                                                          last ? coin_mode : 0);
       lvl /= cnt * 2;
       continue;
     }
@@ -543,28 +565,6 @@ void launch_merkle(fe* d_nodes, size_t n, hipStream_t s) {
       merkle_level_kernel<<<pg_blocks(lvl), 256, 0, s>>>(d_nodes, lvl);
     lvl /= 2;
   }
-}
-
-// FRI transcript step on the device (DefaultRandomCoin: reseed with the layer root, then
-// draw alpha with counter 1): coin[0] = merge(coin[0], root); coin[1] = merge_with_int(
-// coin[0], 1); the root is also copied to *root_out.  One wave, group 0.
-__global__ __launch_bounds__(64) void fri_coin_kernel(fe* coin, const fe* root, fe* root_out) {
-  __shared__ __align__(16) uint32_t pw_lds[PW_WAVE_WORDS];
-  PWGroup P;
-  pw_init(P, pw_lds);
-  const bool live = P.g == 0;
-  const fe seed = coin[0], r = *root;
-  fe s1 = pw_sponge<DOM_MERGE>(P, live, 2, [&](int j) { return j == 0 ? seed : r; });
-  s1 = pw_bcast(P, s1, 0);
-  fe a = pw_sponge<DOM_INT>(P, live, 2, [&](int j) { return j == 0 ? s1 : fe{1, 0}; });
-  if (threadIdx.x == 0) {
-    coin[0] = s1;
-    coin[1] = a;
-    *root_out = r;
-  }
-}
-void launch_fri_coin(fe* d_coin, const fe* d_root, fe* d_root_out, hipStream_t s) {
-  fri_coin_kernel<<<1, 64, 0, s>>>(d_coin, d_root, d_root_out);
 }
 
 __global__ PG_KERNEL void pg_permute_kernel(fe* st, size_t n) {
@@ -602,23 +602,8 @@ void launch_grind(fe seed, uint64_t base, uint32_t count, uint32_t bits, unsigne
 }
 
 // ---- device transcript steps (DefaultRandomCoin on the device; one wave, group 0) --------
-// coin[0] = merge(coin[0], *v); *v_out = *v (the commitment, for the proof bytes)
-__global__ __launch_bounds__(64) void coin_reseed_kernel(fe* coin, const fe* v, fe* v_out) {
-  __shared__ __align__(16) uint32_t pw_lds[PW_WAVE_WORDS];
-  PWGroup P;
-  pw_init(P, pw_lds);
-  const bool live = P.g == 0;
-  const fe seed = coin[0], r = *v;
-  const fe s1 = pw_sponge<DOM_MERGE>(P, live, 2, [&](int j) { return j == 0 ? seed : r; });
-  if (threadIdx.x == 0) {
-    coin[0] = s1;
-    if (v_out) *v_out = r;
-  }
-}
-void launch_coin_reseed(fe* d_coin, const fe* d_value, fe* d_value_out, hipStream_t s) {
-  coin_reseed_kernel<<<1, 64, 0, s>>>(d_coin, d_value, d_value_out);
-}
-
+// (the reseeds after the trace, constraint and FRI layer trees run in the tree's last launch,
+// merkle_top_kernel's coin_mode)
 // FRI remainder (agg/trace.rs:926-952 geometry): the rlen lowest coefficients of the Nr last
 // evaluations over 3 <w_Nr> (c_k = sum_j ev_j w^-jk / Nr * 3^-k), stored highest degree first
 // in rem[0..rlen), rem[rlen] = hash_elements(rem), then coin[0] = merge(coin[0], rem[rlen]).

@@ -498,13 +498,8 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     launch_hash_rows(C->lde.f(), W, N, o.num_partitions, o.hash_rate, C->parts.f(), C->tree.f() + N, s, 0, split);
   }
   check_launch("trace row hash");
-  {
-    KScope k(C, KF_MERKLE);
-    launch_merkle(C->tree.f(), N, s);
-  }
-  check_launch("trace Merkle tree");
   // ---- coin seed: Context::to_elements || AirPublicInputs::to_elements (agg/fs.rs:67-73),
-  // hashed on the host while the device runs the trace LDE and commitment queued above
+  // hashed on the host while the device runs the trace LDE and row hash queued above
   std::vector<fe> seed_el = context_elements(W, n, o);
   auto pie = pi_elements(pi);
   seed_el.insert(seed_el.end(), pie.begin(), pie.end());
@@ -521,8 +516,11 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   fe* htx = C->h_tx.at<fe>();
   htx[32] = coin.seed;
   HIPCHECK(hipMemcpyAsync(tx, htx + 32, sizeof(fe), hipMemcpyHostToDevice, s));
-  launch_coin_reseed(tx, C->tree.f() + 1, tx + 2, s);
-  check_launch("trace-root reseed");
+  {
+    KScope k(C, KF_MERKLE);
+    launch_merkle(C->tree.f(), N, s, tx, tx + 2, 1);  // + the trace-root reseed
+  }
+  check_launch("trace Merkle tree and trace-root reseed");
   coin.counter = 0;  // coin.seed is on the device until the constraint root
   // The AIR instance (layout, degrees, ~2.9e5 assertions at n = 2^16) is built on the host
   // meanwhile too.
@@ -685,9 +683,8 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   }
   {
     KScope k(C, KF_MERKLE);
-    launch_merkle(C->ctree.f(), N, s);
+    launch_merkle(C->ctree.f(), N, s, tx, tx + 3, 1);  // + the constraint-root reseed
   }
-  launch_coin_reseed(tx, C->ctree.f() + 1, tx + 3, s);
   check_launch("composition commitment");
   // one round trip: degree flag, both roots and the coin seed after the constraint root
   HIPCHECK(hipMemcpyAsync(htx, tx, 4 * sizeof(fe), hipMemcpyDeviceToHost, s));
@@ -805,10 +802,9 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
     }
     {
       KScope k(C, KF_MERKLE);
-      launch_merkle(tr, h, s);
+      launch_merkle(tr, h, s, d_coin, d_coin + 2 + d, 2);  // + the layer's reseed and alpha
     }
     KScope k(C, KF_FRI);
-    launch_fri_coin(d_coin, tr + 1, d_coin + 2 + d, s);
     launch_fri_fold(layer_ev(d), Nd, d_coin + 1, iroots, Ntab, layer_ev(d + 1), s);
   }
   check_launch("FRI layers");
