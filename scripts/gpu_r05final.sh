@@ -5,7 +5,7 @@
 #                                          headline-only bench, SQ counters and FETCH/WRITE traffic
 set -u
 root=$(pwd)
-tag=r05final
+tag=${ZKL_FINAL_TAG:-r05final}
 out=$root/gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
