@@ -227,7 +227,8 @@ int zkl_hip_hash_rows(zkl_ctx* ctx, const void* d_matrix, uint32_t n_cols, uint3
 int zkl_hip_merkle_tree(zkl_ctx* ctx, const void* d_leaves, uint32_t n_leaves, void* d_nodes_out);
 /* n_states Poseidon permutations (poseidon/hasher.rs:173-190, suite [0;32]) of 12-element
  * canonical states, in place.  engine 1 = matrix-core form (the one the commitment kernels
- * use on large levels), 0 = lane-group form.  Stage entry point for parity tests. */
+ * use on large levels), 2 = its 16-state form (levels of 2^13 and 2^14 states), 0 = lane-group
+ * form.  Stage entry point for parity tests. */
 int zkl_hip_poseidon_permute(zkl_ctx* ctx, void* d_states, uint32_t n_states, int engine);
 /* Process-wide hashing policy: engine 1 (default) runs Poseidon levels of at least
  * pm_min_items states (default 16384) on the matrix-core permutation, engine 0 keeps every

@@ -430,9 +430,9 @@ def _fe_buf(vals):
     return (C.c_uint8 * (16 * len(vals))).from_buffer_copy(b"".join(v.to_bytes(16, "little") for v in vals))
 
 
-@pytest.mark.parametrize("engine", [1, 0])
+@pytest.mark.parametrize("engine", [1, 0, 2])
 def test_stage_permute_matches_oracle(oracle, gpu_ctx, engine):
-    """zkl_hip_poseidon_permute (both permutation forms) vs the oracle permutation, on
+    """zkl_hip_poseidon_permute (the 32- and 16-state matrix-core forms, the lane-group form) vs the oracle permutation, on
     random states, a partial last batch and the extreme elements 0, 1, p-1, 2^127."""
     rng = random.Random(11 + engine)
     P = oracle.P

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -381,6 +382,24 @@ static inline unsigned pw_blocks(size_t items) {
 #endif
 constexpr size_t PW_MAX_ITEMS = PW_MAX_ITEMS_CFG;
 
+// levels (and FRI layers) of [lo, hi) states use the 16-state matrix-core form (with the
+// matrix-core engine): there the 32-state form runs at most half a wave per SIMD (2^14 states)
+// and the lane groups a wave on every other SIMD (2^13), so a level costs one permutation's
+// latency, which the 16-state form, with half the VALU work per lane, shortens: 2^14 states
+// 69.5 -> 47 us, 2^13 56 -> 47 us (lane groups); at 2^15 the 32-state form is faster (73 against
+// 80 us, profiles/r05/pm16/).  ZKL_PM16=lo,hi (0 = off) for A/B; default 2^13, 2^15.
+static bool pm16_range(size_t items) {
+  static const size_t* lim = [] {
+    static size_t v[2] = {(size_t)1 << 13, (size_t)1 << 15};
+    if (const char* e = getenv("ZKL_PM16")) {
+      if (!strcmp(e, "0")) v[0] = v[1] = 0;
+      else if (sscanf(e, "%zu,%zu", &v[0], &v[1]) != 2) throw std::invalid_argument("ZKL_PM16: expected lo,hi");
+    }
+    return v;
+  }();
+  return items >= lim[0] && items < lim[1];
+}
+
 // Occupancy target of the lane-group kernels: 2 waves/SIMD lets the scheduler batch the 15
 // LDS reads of a round; 3 forces them to serialise on a shared register window.
 #ifndef PG_WAVES
@@ -559,7 +578,9 @@ void launch_merkle(fe* d_nodes, size_t n, hipStream_t s, fe* d_coin, fe* d_root_
       lvl /= cnt * 2;
       continue;
     }
-    if (hash_engine() == 1 && lvl >= pm_min_items())
+    if (hash_engine() == 1 && pm16_range(lvl))
+      PM16_GO(merkle_level_pm16_kernel, lvl, s)(d_nodes, lvl);
+    else if (hash_engine() == 1 && lvl >= pm_min_items())
       PM_GO(merkle_level_pm_kernel, lvl, false, s)(d_nodes, lvl);
     else
       merkle_level_kernel<<<pg_blocks(lvl), 256, 0, s>>>(d_nodes, lvl);
@@ -579,7 +600,9 @@ __global__ PG_KERNEL void pg_permute_kernel(fe* st, size_t n) {
 
 void launch_permute(fe* d_states, size_t n, int engine, hipStream_t s) {
   if (!n) return;
-  if (engine == 1)
+  if (engine == 2)
+    PM16_GO(pm16_permute_kernel, n, s)(d_states, n);
+  else if (engine == 1)
     PM_GO(pm_permute_kernel, n, false, s)(d_states, n);
   else
     pg_permute_kernel<<<pg_blocks(n), 256, 0, s>>>(d_states, n);
@@ -683,6 +706,8 @@ void launch_fri_leaves(const fe* d_ev, size_t Nd, fe* d_leaves, hipStream_t s) {
   size_t h = Nd / 2;
   if (h <= PW_MAX_ITEMS)
     fri_leaf_wide_kernel<<<pw_blocks(h), 256, 0, s>>>(d_ev, h, d_leaves);
+  else if (hash_engine() == 1 && pm16_range(h))
+    PM16_GO(fri_leaf_pm16_kernel, h, s)(d_ev, h, d_leaves);
   else if (hash_engine() == 1 && h >= pm_min_items())
     PM_GO(fri_leaf_pm_kernel, h, false, s)(d_ev, h, d_leaves);
   else

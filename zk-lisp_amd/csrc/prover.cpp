@@ -1386,7 +1386,7 @@ int zkl_hip_set_hash_policy(int engine, uint32_t pm_min_items) {
 }
 
 int zkl_hip_poseidon_permute(zkl_ctx* c, void* d_states, uint32_t n_states, int engine) {
-  if (!c || !d_states || engine < 0 || engine > 1) return ZKL_E_INVALID;
+  if (!c || !d_states || engine < 0 || engine > 2) return ZKL_E_INVALID;
   std::lock_guard<std::mutex> lk(c->mu);
   return run_guarded(c, [&] {
     HIPCHECK(hipSetDevice(c->device));
