@@ -35,6 +35,114 @@ __global__ __launch_bounds__(512) void pw_chain_kernel(fe* io, int reps, int act
   }
 }
 
+// Parts of the 48-lane round, each timed as a chain of 27 x reps rounds on one wave:
+// MODE 1 = the cube alone, 2 = the cube exchange through LDS alone, 3 = exchange + MDS columns
+// + fold + DPP sums (no cube), 0 = the whole round (as pw_permute), 4 = the whole round with
+// two of the three MDS columns per lane (50 instead of 75 multiply-adds; timing only), 5 / 6 =
+// 0 / 2 with the cubes gathered by ds_bpermute instead of an LDS store and load, 7 / 9 = 0 / 2
+// with the cubes laid out so that a lane's 15 words are four 128-bit reads, 8 = a copy of 0
+// (code-placement noise).
+template <int MODE>
+__global__ __launch_bounds__(64) void pw_part_kernel(fe* io, int reps, unsigned long long* cyc) {
+  __shared__ __align__(16) uint32_t pw_lds[2 * 64];  // room for the 64-word layout of MODE 7 / 9
+  PWGroup P;
+  pw_init(P, pw_lds);
+  uint32_t s[5];
+  to_mont130(io[threadIdx.x & 63], s);
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < reps; i++) {
+    const uint32_t* rcp = &c_hm.rc130[0][P.e][0];
+#pragma unroll 1
+    for (int r = 0; r < 27; r++, rcp += 60) {
+      uint32_t rc[5];
+#pragma unroll
+      for (int l = 0; l < 5; l++) rc[l] = rcp[l];
+      uint32_t t[5];
+      if (MODE == 2 || MODE == 3 || MODE == 6 || MODE == 9) {
+#pragma unroll
+        for (int l = 0; l < 5; l++) t[l] = s[l];
+      } else {
+        mont_cube130(s, t);
+      }
+      if (MODE == 1) {
+#pragma unroll
+        for (int l = 0; l < 5; l++) s[l] = t[l] + rc[l];
+        continue;
+      }
+      uint32_t tk[PW_COLS][5];
+      if (MODE == 7 || MODE == 9) {  // LDS, the 15 words a lane reads contiguous: 4 x 128-bit reads
+        // element k at word 16 (k / 3) + 5 (k % 3) + l
+        if (P.h == 0) {
+          uint32_t* w = P.x + 16 * (P.e / 3) + 5 * (P.e % 3);
+#pragma unroll
+          for (int l = 0; l < 5; l++) w[l] = t[l];
+        }
+        wave_sync();
+        const uint4* r = reinterpret_cast<const uint4*>(P.x + 16 * P.h);
+        uint32_t v[16];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint4 a = r[q];
+          v[4 * q] = a.x; v[4 * q + 1] = a.y; v[4 * q + 2] = a.z; v[4 * q + 3] = a.w;
+        }
+#pragma unroll
+        for (int k = 0; k < PW_COLS; k++)
+#pragma unroll
+          for (int l = 0; l < 5; l++) tk[k][l] = v[5 * k + l];
+        __builtin_amdgcn_wave_barrier();
+      } else if (MODE == 5 || MODE == 6) {  // cross-lane reads instead of the LDS round trip
+        const int base = PW_LANES * P.g + P.h;
+#pragma unroll
+        for (int k = 0; k < PW_COLS; k++) {
+          const int addr = ((base + PW_SPLIT * (PW_COLS * P.h + k)) & 63) << 2;
+#pragma unroll
+          for (int l = 0; l < 5; l++) tk[k][l] = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)t[l]);
+        }
+      } else {
+        if (P.h == 0) {
+#pragma unroll
+          for (int l = 0; l < 5; l++) P.x[l * 12 + P.e] = t[l];
+        }
+        wave_sync();
+#pragma unroll
+        for (int l = 0; l < 5; l++)
+#pragma unroll
+          for (int k = 0; k < PW_COLS; k++) tk[k][l] = P.x[l * 12 + PW_COLS * P.h + k];
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (MODE == 2 || MODE == 6 || MODE == 9) {
+#pragma unroll
+        for (int l = 0; l < 5; l++) s[l] = (tk[0][l] ^ tk[1][l] ^ tk[2][l]) + rc[l];
+        continue;
+      }
+      uint64_t col[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < (MODE == 4 ? PW_COLS - 1 : PW_COLS); k++)
+#pragma unroll
+        for (int u = 0; u < 5; u++)
+#pragma unroll
+          for (int l = 0; l < 5; l++) col[l] += (uint64_t)tk[k][u] * P.c[k][u][l];
+      uint32_t part[5];
+      pw_fold(col, part);
+#pragma unroll
+      for (int l = 0; l < 5; l++) s[l] = pw_elem_sum(part[l]) + rc[l];
+    }
+  }
+  const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+  io[threadIdx.x & 63] = from_mont130(s);
+  if (threadIdx.x == 0) cyc[0] = c1 - c0;
+}
+
+template <int MODE>
+static void part_run(fe* io, unsigned long long* cyc, int reps, hipStream_t s, const char* what) {
+  pw_part_kernel<MODE><<<1, 64, 0, s>>>(io, 2, cyc);
+  pw_part_kernel<MODE><<<1, 64, 0, s>>>(io, reps, cyc);
+  ZKL_HIPCHECK(hipStreamSynchronize(s));
+  unsigned long long c = 0;
+  ZKL_HIPCHECK(hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost));
+  printf("{\"part\": \"%s\", \"cycles_per_round\": %.1f}\n", what, (double)c / reps / 27);
+}
+
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 200;
   HasherConsts hc{};
@@ -85,5 +193,16 @@ int main(int argc, char** argv) {
            "\"cycles_per_perm\": %.0f, \"cycles_per_round\": %.1f, \"clock_mhz\": %.0f}\n",
            c.what, reps, ms * 1e3 / reps, rt / 100.0 / reps, cy / reps, cy / reps / 27, cy / (rt / 100.0));
   }
+  part_run<0>(io, cyc, reps, s, "whole round");
+  part_run<1>(io, cyc, reps, s, "cube");
+  part_run<2>(io, cyc, reps, s, "LDS exchange");
+  part_run<3>(io, cyc, reps, s, "exchange + MDS + fold + sums");
+  part_run<4>(io, cyc, reps, s, "whole round, 50 MDS multiply-adds");
+  part_run<5>(io, cyc, reps, s, "whole round, bpermute exchange");
+  part_run<6>(io, cyc, reps, s, "bpermute exchange");
+  part_run<7>(io, cyc, reps, s, "whole round, 128-bit reads");
+  part_run<9>(io, cyc, reps, s, "128-bit-read exchange");
+  part_run<8>(io, cyc, reps, s, "whole round (copy)");
+  part_run<0>(io, cyc, reps, s, "whole round (again)");
   return 0;
 }
