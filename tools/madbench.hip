@@ -1,6 +1,6 @@
 // Issue/latency microbenchmark of the integer multiply forms used by the field arithmetic
 // (gfx950): v_mad_u64_u32, v_mul_lo_u32, v_mad_u32_u24, v_mul_hi_u32_u24, v_dot2_u32_u16,
-// v_fma_f64.  One wave (latency view: one wave per SIMD, no other wave to hide behind) and a
+// v_fma_f64, the 64-bit shifts and the 32-bit ops of the carries (round 5).  One wave (latency view: one wave per SIMD, no other wave to hide behind) and a
 // full chip (throughput view).  Prints shader cycles and ns per wave-instruction.
 //   hipcc --offload-arch=gfx950 -O3 tools/madbench.hip -o /tmp/madbench && /tmp/madbench
 #include <hip/hip_runtime.h>
@@ -62,6 +62,30 @@ __global__ void bench(uint64_t* out, uint32_t seed) {
 #define OPI(i) asm volatile("v_lshl_add_u64 %0, %0, 2, %1" : "+v"(acc[DEP ? 0 : i]) : "v"(acc[(i + 1) & 7]));
       CHAIN8(OPI)
 #undef OPI
+    } else if (KIND == 8) {  // v_ashrrev_i64 (the REDC / fold carries)
+#define OPI(i) asm volatile("v_ashrrev_i64 %0, 3, %0" : "+v"(acc[DEP ? 0 : i]));
+      CHAIN8(OPI)
+#undef OPI
+    } else if (KIND == 9) {  // v_lshrrev_b64
+#define OPI(i) asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(acc[DEP ? 0 : i]));
+      CHAIN8(OPI)
+#undef OPI
+    } else if (KIND == 10) {  // v_mad_i64_i32 (digit-column fold, REDC's -2^24 m)
+#define OPI(i) asm volatile("v_mad_i64_i32 %0, vcc, %1, %2, %0" : "+v"(acc[DEP ? 0 : i]) : "v"(a[i]), "v"(b) : "vcc");
+      CHAIN8(OPI)
+#undef OPI
+    } else if (KIND == 11) {  // v_alignbit_b32 (a 64-bit shift's low word in one 32-bit op)
+#define OPI(i) asm volatile("v_alignbit_b32 %0, %1, %0, 26" : "+v"(a[DEP ? 0 : i]) : "v"(b));
+      CHAIN8(OPI)
+#undef OPI
+    } else if (KIND == 12) {  // v_and_b32
+#define OPI(i) asm volatile("v_and_b32 %0, %1, %0" : "+v"(a[DEP ? 0 : i]) : "v"(b));
+      CHAIN8(OPI)
+#undef OPI
+    } else if (KIND == 13) {  // v_mad_u64_u32 and v_add_u32 alternating (independent)
+#define OPI(i) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0\n v_add_u32 %3, %2, %3" : "+v"(acc[i]), "+v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(b) : "vcc");
+      CHAIN8(OPI)
+#undef OPI
     }
   }
   const uint64_t c1 = clock64(), w1 = wall_clock64();
@@ -75,7 +99,9 @@ __global__ void bench(uint64_t* out, uint32_t seed) {
 }
 
 static const char* names[] = {"v_mad_u64_u32", "v_mul_lo_u32", "v_mad_u32_u24", "v_mul_hi_u32_u24",
-                              "v_dot2_u32_u16", "v_fma_f64", "v_add_u32", "v_lshl_add_u64"};
+                              "v_dot2_u32_u16", "v_fma_f64", "v_add_u32", "v_lshl_add_u64",
+                              "v_ashrrev_i64", "v_lshrrev_b64", "v_mad_i64_i32", "v_alignbit_b32",
+                              "v_and_b32", "mad_u64+add_u32"};
 
 template <int K, bool D>
 static void run(uint64_t* d, int blocks, int threads) {
@@ -91,7 +117,7 @@ static void run(uint64_t* d, int blocks, int threads) {
   float ms = 0;
   (void)hipEventElapsedTime(&ms, e0, e1);
   (void)hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);
-  const double n_instr = 8.0 * ITERS;
+  const double n_instr = (K == 13 ? 16.0 : 8.0) * ITERS;
   int wall_mhz = 0;
   (void)hipDeviceGetAttribute(&wall_mhz, hipDeviceAttributeWallClockRate, 0);  // kHz
   const double wall_ns = (double)h[1] * 1e6 / (double)wall_mhz;
@@ -106,6 +132,8 @@ static void kind(uint64_t* d, int cus) {
   run<K, false>(d, 1, 64);
   run<K, true>(d, 1, 64);
   run<K, false>(d, cus, 256);      // one wave per SIMD everywhere
+  run<K, false>(d, cus * 2, 256);  // 2 waves per SIMD
+  run<K, false>(d, cus * 3, 256);  // 3 waves per SIMD
   run<K, false>(d, cus * 8, 256);  // 8 waves per SIMD
 }
 
@@ -123,6 +151,12 @@ int main() {
   kind<5>(d, cus);
   kind<6>(d, cus);
   kind<7>(d, cus);
+  kind<8>(d, cus);
+  kind<9>(d, cus);
+  kind<10>(d, cus);
+  kind<11>(d, cus);
+  kind<12>(d, cus);
+  kind<13>(d, cus);
   (void)hipFree(d);
   return 0;
 }
