@@ -263,6 +263,33 @@ def test_stage_hash_rows_and_merkle(oracle, gpu_ctx):
         gpu_ctx.free(d)
 
 
+def test_stage_merkle_every_level_form(oracle, gpu_ctx):
+    """A 2^17-leaf tree walks every level form launch_merkle picks (poseidon.hip:571-589): the
+    32-state matrix-core levels (2^16, 2^15 nodes), the 16-state ones (2^14, 2^13), a lane-group
+    level (2^12) and the 48-lane tree tops (<= 2^11, three launches); every node is compared with
+    the oracle's merge (hasher.rs merge), not only the root."""
+    rng = random.Random(17)
+    P = oracle.P
+    n = 1 << 17
+    leaves = [rng.randrange(P) for _ in range(n)]
+    raw = (C.c_uint8 * (16 * n)).from_buffer_copy(b"".join(v.to_bytes(16, "little") for v in leaves))
+    d_l = gpu_ctx.alloc(16 * n)
+    d_nodes = gpu_ctx.alloc(2 * n * 16)
+    gpu_ctx.upload(d_l, raw, len(raw))
+    gpu_ctx.merkle_tree(d_l, n, d_nodes)
+    nodes = gpu_ctx.download(d_nodes, 2 * n * 16)
+    got = [int.from_bytes(nodes[16 * i:16 * i + 16], "little") for i in range(2 * n)]
+    assert got[n:] == leaves
+    lvl, base = leaves, n
+    while base > 1:
+        lvl = [oracle.merge(lvl[2 * i], lvl[2 * i + 1]) for i in range(len(lvl) // 2)]
+        base //= 2
+        bad = [i for i in range(base) if got[base + i] != lvl[i]]
+        assert not bad, f"level of {base} nodes: {len(bad)} nodes differ, first {bad[:4]}"
+    for d in (d_l, d_nodes):
+        gpu_ctx.free(d)
+
+
 @pytest.mark.parametrize("log_n,blow", [(6, 16), (6, 8), (6, 2), (5, 32), (9, 4)])
 def test_stage_lde_matches_oracle(oracle, gpu_ctx, log_n, blow):
     """zkl_hip_lde: coefficients and coset LDE (GENERATOR * <w_{blow*n}>) vs direct evaluation."""
