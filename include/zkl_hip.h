@@ -171,6 +171,20 @@ int zkl_hip_prove_segment_device(zkl_ctx* ctx, const void* d_trace, uint32_t wid
                                  const zkl_air_public_inputs* pi, const zkl_proof_options* opts,
                                  uint8_t** proof_out, size_t* proof_len);
 
+/* The same proof written into caller memory (no allocation, one copy): for a binding that keeps
+ * one buffer across segments (e.g. a Vec<u8> reserved once and set_len'd; the reference's
+ * Proof::to_bytes at prove.rs:1142 allocates per proof).  *proof_len receives the size; with
+ * cap too small (or buf NULL, a size query) the call returns ZKL_E_INVALID (NULL: ZKL_OK) and
+ * the bytes stay on the context for zkl_hip_last_proof. */
+int zkl_hip_prove_segment_device_into(zkl_ctx* ctx, const void* d_trace, uint32_t width, uint32_t n_rows,
+                                      const zkl_air_public_inputs* pi, const zkl_proof_options* opts,
+                                      uint8_t* buf, size_t cap, size_t* proof_len);
+
+/* The last proof made on ctx (any zkl_hip_prove_segment* call), valid until the next one:
+ * *len = its size; copied into buf when buf != NULL and cap >= *len (ZKL_E_INVALID when cap is
+ * too small or no proof is held). */
+int zkl_hip_last_proof(zkl_ctx* ctx, uint8_t* buf, size_t cap, size_t* len);
+
 /* The request checks zkl_hip_prove_segment* run before any device work, without a device:
  * ProofOptions / PartitionOptions bounds (num_queries 1..255, blowup a power of two >= 2 and
  * >= the AIR's constraint-evaluation blowup, num_partitions 1..16, hash_rate 1..256, FRI

@@ -883,6 +883,37 @@ def test_host_trace_chunked_upload_matches_device_entry(gpu_ctx, log_n, width_fl
     zkl_hip.verify_segment(host, pi, opts)
 
 
+def test_prove_into_caller_buffer(gpu_ctx):
+    """zkl_hip_prove_segment_device_into writes the same bytes zkl_hip_prove_segment_device
+    returns; a buffer one byte short fails with the size named and zkl_hip_last_proof still
+    returns the proof; after a failed prove call no proof is held."""
+    import zkl_hip
+    log_n = 12
+    n = 1 << log_n
+    t, pi, w = zkl_hip.synth_vm_segment(0x5EED1700, log_n, 0)
+    opts = zkl_hip.proof_options(w, n, queries=16, grind=4)
+    d = gpu_ctx.alloc(w * n * 16)
+    try:
+        gpu_ctx.upload(d, t, w * n * 16)
+        ref = gpu_ctx.prove_segment_device(d, w, n, pi, opts)
+        assert gpu_ctx.last_proof() == ref
+        buf = bytearray(len(ref) + 100)
+        ln = gpu_ctx.prove_segment_device_into(d, w, n, pi, opts, buf)
+        assert ln == len(ref) and bytes(buf[:ln]) == ref
+        short = bytearray(len(ref) - 1)
+        with pytest.raises(zkl_hip.ZklError, match=f"{len(ref)} bytes needed"):
+            gpu_ctx.prove_segment_device_into(d, w, n, pi, opts, short)
+        assert gpu_ctx.last_proof() == ref
+        bad = zkl_hip.proof_options(w, n, queries=16, grind=4)
+        bad.blowup_factor = 3  # not a power of two: rejected before any device work
+        with pytest.raises(zkl_hip.ZklError):
+            gpu_ctx.prove_segment_device_into(d, w, n, pi, bad, buf)
+        with pytest.raises(zkl_hip.ZklError, match="no proof"):
+            gpu_ctx.last_proof()
+    finally:
+        gpu_ctx.free(d)
+
+
 @pytest.mark.parametrize("flags,blowup", [(0, 8), (0, 16), (0, 32), (0, 64), (1, 16), (2, 8)])
 def test_split_lde_layout_proofs_match_oracle(oracle, gpu_ctx, flags, blowup):
     """2^8-row segments are the smallest whose trace LDE ends in an 8-stage register pass, so

@@ -440,8 +440,9 @@ struct InFlight {
   ~InFlight() { g_proofs_in_flight.fetch_sub(1); }
 };
 
+// the proof bytes are left in C->proof_s (zkl_hip_last_proof), valid until the next proof
 void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t W, uint32_t n32,
-                const zkl_air_public_inputs& pi, const zkl_proof_options& o, std::vector<uint8_t>& out) {
+                const zkl_air_public_inputs& pi, const zkl_proof_options& o) {
   const InFlight in_flight;
   const auto t_call0 = std::chrono::steady_clock::now();
   hipStream_t s = C->stream;
@@ -1043,7 +1044,6 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   T.finish();
   HT("stage_events");
   resolve_kernel_times(C);
-  out.assign(P.v.begin(), P.v.end());
   C->proof_s.swap(P.v);
   HT("returned");
   C->host_ms[2] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call0).count();
@@ -1201,12 +1201,12 @@ int zkl_hip_prove_segment(zkl_ctx* c, const zkl_f128* trace, uint32_t width, uin
                           const zkl_proof_options* o, uint8_t** proof, size_t* len) {
   if (!c || !trace || !pi || !o || !proof || !len) return ZKL_E_INVALID;
   std::lock_guard<std::mutex> lk(c->mu);
-  std::vector<uint8_t> v;
+  c->proof_s.clear();
   int rc = run_guarded(c, [&] {
     HIPCHECK(hipSetDevice(c->device));
-    prove_impl(c, trace, true, width, n, *pi, *o, v);
+    prove_impl(c, trace, true, width, n, *pi, *o);
   });
-  return rc ? rc : finish_proof(v, proof, len);
+  return rc ? rc : finish_proof(c->proof_s, proof, len);
 }
 
 int zkl_hip_prove_segment_device(zkl_ctx* c, const void* d_trace, uint32_t width, uint32_t n,
@@ -1214,12 +1214,48 @@ int zkl_hip_prove_segment_device(zkl_ctx* c, const void* d_trace, uint32_t width
                                  size_t* len) {
   if (!c || !d_trace || !pi || !o || !proof || !len) return ZKL_E_INVALID;
   std::lock_guard<std::mutex> lk(c->mu);
-  std::vector<uint8_t> v;
+  c->proof_s.clear();
   int rc = run_guarded(c, [&] {
     HIPCHECK(hipSetDevice(c->device));
-    prove_impl(c, d_trace, false, width, n, *pi, *o, v);
+    prove_impl(c, d_trace, false, width, n, *pi, *o);
   });
-  return rc ? rc : finish_proof(v, proof, len);
+  return rc ? rc : finish_proof(c->proof_s, proof, len);
+}
+
+// copy of the context's last proof into caller memory (no allocation); caller holds c->mu
+static int copy_last_proof(zkl_ctx* c, uint8_t* buf, size_t cap, size_t* len) {
+  *len = c->proof_s.size();
+  if (c->proof_s.empty()) {
+    c->err = "no proof on this context (the last prove call failed or none was made)";
+    return ZKL_E_INVALID;
+  }
+  if (!buf) return ZKL_OK;  // size query
+  if (cap < c->proof_s.size()) {
+    c->err = "proof buffer too small: " + std::to_string(c->proof_s.size()) + " bytes needed, " +
+             std::to_string(cap) + " given (zkl_hip_last_proof still returns it)";
+    return ZKL_E_INVALID;
+  }
+  memcpy(buf, c->proof_s.data(), c->proof_s.size());
+  return ZKL_OK;
+}
+
+int zkl_hip_last_proof(zkl_ctx* c, uint8_t* buf, size_t cap, size_t* len) {
+  if (!c || !len) return ZKL_E_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  return copy_last_proof(c, buf, cap, len);
+}
+
+int zkl_hip_prove_segment_device_into(zkl_ctx* c, const void* d_trace, uint32_t width, uint32_t n,
+                                      const zkl_air_public_inputs* pi, const zkl_proof_options* o, uint8_t* buf,
+                                      size_t cap, size_t* len) {
+  if (!c || !d_trace || !pi || !o || !len) return ZKL_E_INVALID;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->proof_s.clear();
+  int rc = run_guarded(c, [&] {
+    HIPCHECK(hipSetDevice(c->device));
+    prove_impl(c, d_trace, false, width, n, *pi, *o);
+  });
+  return rc ? rc : copy_last_proof(c, buf, cap, len);
 }
 
 int zkl_hip_check_request(uint32_t width, uint32_t n_rows, const zkl_air_public_inputs* pi,

@@ -126,6 +126,10 @@ def load_library():
     lib.zkl_hip_prove_segment.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                           P(AirPublicInputs), P(ProofOptions), P(P(C.c_uint8)), P(C.c_size_t)]
     lib.zkl_hip_prove_segment_device.argtypes = lib.zkl_hip_prove_segment.argtypes
+    lib.zkl_hip_prove_segment_device_into.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                                      P(AirPublicInputs), P(ProofOptions), C.c_void_p, C.c_size_t,
+                                                      P(C.c_size_t)]
+    lib.zkl_hip_last_proof.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, P(C.c_size_t)]
     lib.zkl_hip_stage_times.argtypes = [C.c_void_p, P(C.c_double), C.c_int]
     lib.zkl_hip_host_times.argtypes = [C.c_void_p, P(C.c_double), C.c_int]
     lib.zkl_hip_kernel_times.argtypes = [C.c_void_p, P(C.c_double), P(C.c_int), C.c_int, P(C.c_char_p)]
@@ -620,6 +624,30 @@ class Context:
         rc = self.lib.zkl_hip_prove_segment_device(self.ptr, C.c_void_p(d_trace_ptr), width, n_rows, C.byref(pi),
                                                    C.byref(opts), C.byref(out), C.byref(ln))
         return self._finish(rc, out, ln)
+
+    def prove_segment_device_into(self, d_trace_ptr: int, width: int, n_rows: int, pi, opts, buf) -> int:
+        """Same, written into `buf` (a writable ctypes / bytearray buffer kept across calls):
+        returns the proof length; a buffer too small raises with the size in the message, and
+        last_proof() still returns the bytes."""
+        ln = C.c_size_t()
+        cbuf = (C.c_uint8 * len(buf)).from_buffer(buf)
+        rc = self.lib.zkl_hip_prove_segment_device_into(self.ptr, C.c_void_p(d_trace_ptr), width, n_rows, C.byref(pi),
+                                                        C.byref(opts), cbuf, len(buf), C.byref(ln))
+        if rc:
+            self._err(rc)
+        return ln.value
+
+    def last_proof(self) -> bytes:
+        """The last proof made on this context (valid until the next prove call)."""
+        ln = C.c_size_t()
+        rc = self.lib.zkl_hip_last_proof(self.ptr, None, 0, C.byref(ln))
+        if rc:
+            self._err(rc)
+        buf = (C.c_uint8 * ln.value)()
+        rc = self.lib.zkl_hip_last_proof(self.ptr, buf, ln.value, C.byref(ln))
+        if rc:
+            self._err(rc)
+        return bytes(buf)
 
     def stage_times(self):
         arr = (C.c_double * len(STAGE_NAMES))()
