@@ -216,6 +216,21 @@ class ZkProver {
                   dev_->ctx());
     return Proof{detail::take(out, len)};
   }
+  // same, the bytes written into `out` (resized; its capacity is kept across calls, so a
+  // caller proving many segments allocates once): zkl_hip_prove_segment_device_into
+  void prove_device_into(const void* d_trace, uint32_t width, uint32_t length, std::vector<uint8_t>& out) const {
+    out.resize(out.capacity());
+    size_t len = 0;
+    const int rc = zkl_hip_prove_segment_device_into(dev_->ctx(), d_trace, width, length, &pi_, &opts_.raw(),
+                                                     out.data(), out.size(), &len);
+    if (len > out.size()) {  // too small (or empty: a size query): the bytes stay on the context
+      out.resize(len);
+      detail::check(zkl_hip_last_proof(dev_->ctx(), out.data(), out.size(), &len), dev_->ctx());
+    } else {
+      detail::check(rc, dev_->ctx());
+    }
+    out.resize(len);
+  }
   const ProofOptions& options() const { return opts_; }
 
  private:

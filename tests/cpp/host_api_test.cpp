@@ -140,6 +140,22 @@ int run_gpu(const char* out_path) {
   zkl::BaseElement* tb = dev.trace_buffer(1, (size_t)w * n * sizeof(zkl::BaseElement));
   std::memcpy(tb, s.trace.data(), (size_t)w * n * sizeof(zkl::BaseElement));
   EXPECT(prover.prove_host(tb, w, n).bytes == proof.bytes);
+  // the trace resident in HBM: prove_device, and prove_device_into with an empty vector (the
+  // too-small path through zkl_hip_last_proof) and again with the capacity it kept
+  {
+    void* d = nullptr;
+    const size_t bytes = (size_t)w * n * sizeof(zkl::BaseElement);
+    EXPECT(zkl_hip_device_alloc(dev.ctx(), bytes, &d) == ZKL_OK);
+    EXPECT(zkl_hip_memcpy(dev.ctx(), d, s.trace.data(), bytes, 1) == ZKL_OK);
+    EXPECT(prover.prove_device(d, w, n).bytes == proof.bytes);
+    std::vector<uint8_t> out;
+    prover.prove_device_into(d, w, n, out);
+    EXPECT(out == proof.bytes);
+    const size_t cap = out.capacity();
+    prover.prove_device_into(d, w, n, out);
+    EXPECT(out == proof.bytes && out.capacity() == cap);
+    EXPECT(zkl_hip_device_free(dev.ctx(), d) == ZKL_OK);
+  }
   zkl::verify_proof(proof, s.pi, opts);
   // a corrupted proof is rejected by the verifier with Error::Backend
   zkl::Proof bad = proof;
