@@ -38,7 +38,7 @@ def test_build_carries_only_default_tuning_values():
     lib.zkl_hip_build_config.restype = C.c_char_p
     cfg = dict(kv.split("=") for kv in lib.zkl_hip_build_config().decode().split(";"))
     assert cfg == {"PM_WAVES": "8", "PM_WIDE": "0", "PM_ROW_WAVES": "8", "PM_IGLP": "0", "TAIL_PRIO": "0",
-                   "PW_MAX_ITEMS": "2048", "PM_ROW_BIG": "0", "PM_PAIR": "0", "POSEIDON_SCHED": "default", "NTT_ELEMS": "1024",
+                   "PW_MAX_ITEMS": "2048", "PM_ROW_BIG": "0", "POSEIDON_SCHED": "default", "NTT_ELEMS": "1024",
                    "NTT_THREADS": "256", "CE_WAVES": "3", "CE_POSE_WAVES": "3", "DEEP_PTS": "2",
                    "DEEP_COLS": "4"}
 
