@@ -45,6 +45,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "zk-lisp_amd"))
 
+T_START = time.time()
 METRIC = "segment-proofs/sec at 65536 rows, blowup=16; proof bytes bit-exact vs CPU ref"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SEED0 = 0x5EED0001             # segment seed of rank / segment 0
@@ -687,14 +688,20 @@ def host_fresh(zkl_hip, device, trace, W, n, pi, opts, steps):
     filled, proved, dropped): two contexts in flight, each proof from a newly malloc'd host trace
     (214 MB, filled with a copy of the trace, freed after its proof) -- against the same with the
     contexts' pinned trace buffers (zkl_hip_trace_buffer, two slots, filled in place, nothing
-    allocated per proof).  Per-proof call times: median and slowest / median (stalled proofs,
-    DESIGN.md §6)."""
+    allocated per proof), and a fresh allocation the caller advises onto transparent huge pages
+    (madvise MADV_HUGEPAGE before the fill).  Per-proof call times: median and slowest / median
+    (stalled proofs), and the median of each phase of a call: malloc, fill (the
+    caller's first touch of fresh pages for fresh allocations), the library call
+    (zkl_hip_prove_segment: staging copies, DMA, proof; its upload loop separately) and free."""
     import ctypes as C
     import threading
-    libc = C.CDLL("libc.so.6")
+    libc = C.CDLL("libc.so.6", use_errno=True)
     libc.malloc.restype = C.c_void_p
     libc.malloc.argtypes = [C.c_size_t]
     libc.free.argtypes = [C.c_void_p]
+    libc.posix_memalign.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_size_t]
+    libc.madvise.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
+    MADV_HUGEPAGE = 14
     nbytes = W * n * 16
     ctxs = [zkl_hip.Context(device) for _ in range(2)]
     src = C.addressof(trace)
@@ -705,6 +712,7 @@ def host_fresh(zkl_hip, device, trace, W, n, pi, opts, steps):
 
         def run(mode):
             times = [[] for _ in ctxs]
+            phases = {"malloc": [], "fill": [], "call": [], "upload_loop": [], "free": []}
             bufs = [[c.trace_buffer(nbytes, k) for k in (0, 1)] for c in ctxs] if mode == "pinned" else None
 
             def work(k):
@@ -712,15 +720,29 @@ def host_fresh(zkl_hip, device, trace, W, n, pi, opts, steps):
                     t0 = time.perf_counter()
                     if mode == "pinned":
                         p = bufs[k][j % 2]
+                    elif mode == "thp":
+                        q = C.c_void_p()
+                        if libc.posix_memalign(C.byref(q), 1 << 21, nbytes):
+                            raise MemoryError("posix_memalign of the host trace failed")
+                        p = q.value
+                        libc.madvise(p, nbytes, MADV_HUGEPAGE)
                     else:
                         p = libc.malloc(nbytes)
                         if not p:
                             raise MemoryError("malloc of the host trace failed")
+                    t1 = time.perf_counter()
                     C.memmove(p, src, nbytes)
+                    t2 = time.perf_counter()
                     ctxs[k].prove_segment(p, W, n, pi, opts)
+                    t3 = time.perf_counter()
+                    up = ctxs[k].host_times().get("upload", 0.0)
                     if mode != "pinned":
                         libc.free(p)
-                    times[k].append((time.perf_counter() - t0) * 1e3)
+                    t4 = time.perf_counter()
+                    times[k].append((t4 - t0) * 1e3)
+                    for key, v in (("malloc", t1 - t0), ("fill", t2 - t1), ("call", t3 - t2), ("free", t4 - t3)):
+                        phases[key].append(v * 1e3)
+                    phases["upload_loop"].append(up)
             th = [threading.Thread(target=work, args=(k,)) for k in range(len(ctxs))]
             t0 = time.perf_counter()
             for x in th:
@@ -732,9 +754,11 @@ def host_fresh(zkl_hip, device, trace, W, n, pi, opts, steps):
             med = flat[len(flat) // 2]
             return {"value": round(len(flat) / dt, 4), "unit": "segment-proofs/s",
                     "ms_per_proof_call_median": round(med, 2), "max_over_median": round(flat[-1] / med, 3),
+                    "phase_ms_median": {k: round(sorted(v)[len(v) // 2], 2) for k, v in phases.items()},
                     "ms_each": [[round(t, 1) for t in ts] for ts in times]}
 
         res["fresh_malloc"] = run("fresh")
+        res["fresh_malloc_hugepages"] = run("thp")
         res["pinned_trace_buffer"] = run("pinned")
     finally:
         for c in ctxs:
@@ -992,6 +1016,13 @@ def main():
         if rank == 0:
             prog_lines[spec] = pl_out
 
+    # per-rank host footprint and wall time (capacity of N ranks on one host)
+    import resource
+    pin_now, pin_peak = zkl_hip.pinned_bytes()
+    ranks_host = dist.gather_to_root({"rank": rank, "device": device, "wall_s": round(time.time() - T_START, 1),
+                                      "max_rss_mb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024),
+                                      "pinned_peak_mb": round(pin_peak / 2**20), "pinned_now_mb": round(pin_now / 2**20)})
+
     if rank == 0:
         value = world * args.steps / elapsed
         dom = max(fam.items(), key=lambda kv: kv[1][0])[0] if fam else "trace_hash_rows"
@@ -1103,6 +1134,7 @@ def main():
                         or pl_out.get("aggregation", {}).get("golden") == "MISMATCH":
                     failures.append(f"program {spec}")
         out["process_tuning"] = tuning
+        out["ranks_host"] = ranks_host
         if world == 1 and args.program_steps > 0:
             try:
                 out["real_program"] = real_program(zkl_hip, device, args.program_steps)

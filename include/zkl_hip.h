@@ -164,6 +164,10 @@ int zkl_hip_prove_segment(zkl_ctx* ctx, const zkl_f128* trace, uint32_t width, u
  * call that grows it. */
 #define ZKL_TRACE_BUFFERS 2
 int zkl_hip_trace_buffer(zkl_ctx* ctx, uint32_t slot, size_t bytes, zkl_f128** out);
+/* Pinned host memory the library holds across all contexts of the process (trace buffers,
+ * upload slots, transcript / gather / proof staging): bytes now and the peak since load.  No
+ * device work; for capacity planning (8 ranks x in-flight contexts on one host). */
+int zkl_hip_pinned_bytes(uint64_t* current, uint64_t* peak);
 
 /* Same, with the trace already resident in HBM (device pointer on ctx's device,
  * column-major).  Used by the multi-segment pipeline and by bench.py. */
@@ -245,8 +249,11 @@ int zkl_hip_merkle_tree(zkl_ctx* ctx, const void* d_leaves, uint32_t n_leaves, v
  * form.  Stage entry point for parity tests. */
 int zkl_hip_poseidon_permute(zkl_ctx* ctx, void* d_states, uint32_t n_states, int engine);
 /* Process-wide hashing policy: engine 1 (default) runs Poseidon levels of at least
- * pm_min_items states (default 16384) on the matrix-core permutation, engine 0 keeps every
- * level on lane groups.  Both give identical digests; this only moves time. */
+ * pm_min_items states (default 16384) on the 32-state matrix-core permutation, and Merkle
+ * levels and FRI leaf layers inside the 16-state band (default [2^13, 2^15) states,
+ * ZKL_PM16=lo,hi moves it, ZKL_PM16=0 disables it) on the 16-state matrix-core form whatever
+ * pm_min_items is; engine 0 keeps every level on lane groups.  All forms give identical
+ * digests; this only moves time. */
 int zkl_hip_set_hash_policy(int engine, uint32_t pm_min_items);
 /* Process-wide row-digest rule for partitioned rows that form a single chunk (partition
  * size > row width: the 7-column composition rows from 2^14 trace rows up, any matrix

@@ -260,6 +260,15 @@ def test_invalid_programs():
         zkl_hip.build_trace([op("Mov", dst=9, src=0), op("End")], PID)
     with pytest.raises(zkl_hip.ZklError):
         zkl_hip.build_trace([op("End")], PID, main_args=[(2, bytes(32))] * 5)
+    # 32-byte ids are checked before the C side reads them
+    with pytest.raises(ValueError):
+        zkl_hip.build_trace([op("End")], PID[:31])
+    with pytest.raises(ValueError):
+        zkl_hip.Program([op("End")], PID, program_commitment=b"short")
+    with pytest.raises(ValueError):
+        zkl_hip.rom_acc_from_program([op("End")], b"")
+    with pytest.raises(ValueError):
+        zkl_hip.children_root(bytes(32), [bytes(32)], [bytes(31)])
 
 
 @pytest.mark.gpu

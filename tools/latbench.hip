@@ -47,8 +47,9 @@ __global__ __launch_bounds__(64) void pw_part_kernel(fe* io, int reps, unsigned 
   __shared__ __align__(16) uint32_t pw_lds[2 * 64];  // room for the 64-word layout of MODE 7 / 9
   PWGroup P;
   pw_init(P, pw_lds);
-  uint32_t s[5];
+  uint32_t s[5], s2[5];
   to_mont130(io[threadIdx.x & 63], s);
+  to_mont130(io[(threadIdx.x + 1) & 63], s2);
   const unsigned long long c0 = __builtin_amdgcn_s_memtime();
   for (int i = 0; i < reps; i++) {
     const uint32_t* rcp = &c_hm.rc130[0][P.e][0];
@@ -58,6 +59,17 @@ __global__ __launch_bounds__(64) void pw_part_kernel(fe* io, int reps, unsigned 
 #pragma unroll
       for (int l = 0; l < 5; l++) rc[l] = rcp[l];
       uint32_t t[5];
+      if (MODE == 10) {  // two independent cube chains per lane: issue-bound or dependency-bound?
+        uint32_t t2[5];
+        mont_cube130(s, t);
+        mont_cube130(s2, t2);
+#pragma unroll
+        for (int l = 0; l < 5; l++) {
+          s[l] = t[l] + rc[l];
+          s2[l] = t2[l] + rc[l];
+        }
+        continue;
+      }
       if (MODE == 2 || MODE == 3 || MODE == 6 || MODE == 9) {
 #pragma unroll
         for (int l = 0; l < 5; l++) t[l] = s[l];
@@ -130,6 +142,7 @@ __global__ __launch_bounds__(64) void pw_part_kernel(fe* io, int reps, unsigned 
   }
   const unsigned long long c1 = __builtin_amdgcn_s_memtime();
   io[threadIdx.x & 63] = from_mont130(s);
+  if (MODE == 10) io[(threadIdx.x & 63) + 64] = from_mont130(s2);
   if (threadIdx.x == 0) cyc[0] = c1 - c0;
 }
 
@@ -195,6 +208,7 @@ int main(int argc, char** argv) {
   }
   part_run<0>(io, cyc, reps, s, "whole round");
   part_run<1>(io, cyc, reps, s, "cube");
+  part_run<10>(io, cyc, reps, s, "two independent cubes per lane (divide by 2)");
   part_run<2>(io, cyc, reps, s, "LDS exchange");
   part_run<3>(io, cyc, reps, s, "exchange + MDS + fold + sums");
   part_run<4>(io, cyc, reps, s, "whole round, 50 MDS multiply-adds");

@@ -9,6 +9,7 @@
 // RCCL is opened at run time (librccl.so.1, the ROCm image's; a process that already holds
 // one, e.g. torch's, shares it), so the library loads and the single-GPU path runs without it.
 #include <dlfcn.h>
+#include <stdio.h>
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
@@ -54,6 +55,7 @@ const Rccl& rccl() {
     // processes on one GPU, which RCCL refuses (duplicate devices)
     const char* alt = getenv("ZKL_RCCL_LIB");
     if (alt && *alt) {
+      fprintf(stderr, "zkl_hip: ZKL_RCCL_LIB=%s replaces librccl (test hook)\n", alt);
       r.h = dlopen(alt, RTLD_NOW | RTLD_LOCAL);
     } else {
       r.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);

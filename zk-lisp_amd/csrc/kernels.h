@@ -49,6 +49,11 @@ struct HasherMont {
   // constants in R' form
   uint32_t mdsl[12][12][5][5];
   uint32_t rc130[27][12][5];
+  // round-1 cubes of the constant state elements of a sponge's first block, packed as the
+  // matrix-core form's B words (four offset-byte words + the top): zero (element with no
+  // message) and the two tag lanes dom130[0], dom130[1] (poseidon_mfma.inc pm_permute)
+  uint32_t pmk0[5];
+  uint32_t pmkt[2][5];
 };
 HasherMont make_hasher_mont(const HasherConsts& h);
 void upload_hasher_mont(const HasherMont& m, hipStream_t s);

@@ -901,26 +901,35 @@ void launch_check_zero_range_bitrev(const fe* d, size_t N, size_t lo, size_t hi,
 // =====================================================================================
 // OOD (TracePolyTable::get_ood_frame / CompositionPoly ood): dot products with powers
 // =====================================================================================
-// partial[(pt * ncols + c) * chunks + k] = sum over chunk k of coef(c, j) * pw_pt[j]; the
-// host adds the chunk partials (the OOD frame is read back anyway)
+// partial[(pt * ncols + c) * chunks + k] = sum over chunk k of coef(c, j) * pw_pt[j] for both
+// points pt = 0 (z) and 1 (z g); the host adds the chunk partials (the OOD frame is read back
+// anyway).  Each coefficient is read once for both dot products (round 6: one launch dimension
+// per point read every coefficient twice, 445 MB per launch for 214 MB of coefficients).
 __global__ __launch_bounds__(256) void ood_kernel(OodArgs A, fe* partial) {
-  const uint32_t c = blockIdx.x, pt = blockIdx.y, k = blockIdx.z;
-  const fe* pw = pt ? A.pw2 : A.pw1;
+  const uint32_t c = blockIdx.x, k = blockIdx.z;
   const fe* col = A.coef + (A.use_off ? (size_t)A.off[c] : (size_t)c * A.col_stride);
   const size_t len = A.n / A.chunks, j0 = (size_t)k * len;
-  uint32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (size_t j = j0 + threadIdx.x; j < j0 + len; j += 256) mul_acc(col[j * A.elem_stride], pw[j], acc);
-  __shared__ fe red[256];
-  red[threadIdx.x] = reduce288(acc);
+  uint32_t acc1[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, acc2[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (size_t j = j0 + threadIdx.x; j < j0 + len; j += 256) {
+    const fe v = col[j * A.elem_stride];
+    mul_acc(v, A.pw1[j], acc1);
+    mul_acc(v, A.pw2[j], acc2);
+  }
+  __shared__ fe red[2][256];
+  red[0][threadIdx.x] = reduce288(acc1);
+  red[1][threadIdx.x] = reduce288(acc2);
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) red[threadIdx.x] = fe_add(red[threadIdx.x], red[threadIdx.x + w]);
+    if ((int)threadIdx.x < w) {
+      red[0][threadIdx.x] = fe_add(red[0][threadIdx.x], red[0][threadIdx.x + w]);
+      red[1][threadIdx.x] = fe_add(red[1][threadIdx.x], red[1][threadIdx.x + w]);
+    }
     __syncthreads();
   }
-  if (threadIdx.x == 0) partial[((size_t)pt * A.ncols + c) * A.chunks + k] = red[0];
+  if (threadIdx.x < 2) partial[((size_t)threadIdx.x * A.ncols + c) * A.chunks + k] = red[threadIdx.x][0];
 }
 void launch_ood(const OodArgs& A, fe* d_partial, hipStream_t s) {
-  ood_kernel<<<dim3(A.ncols, 2, A.chunks), 256, 0, s>>>(A, d_partial);
+  ood_kernel<<<dim3(A.ncols, 1, A.chunks), 256, 0, s>>>(A, d_partial);
 }
 
 // DEEP composition over the LDE domain (agg/trace.rs:1126-1218 restates the formula):

@@ -148,6 +148,16 @@ __host__ __device__ __forceinline__ void mont_cube130(const uint32_t a[5], uint3
   redc130(c2, out);
 }
 
+// a cube's normalised limbs (< 2^131) as the matrix-core permutation's B words: four words of
+// offset bytes (c = sum_j (b_j + 128) 2^(8j) + top 2^128) and the top
+__host__ __device__ __forceinline__ void pm_pack_words(const uint32_t c[5], uint32_t w[5]) {
+  w[0] = (c[0] | (c[1] << 26)) ^ 0x80808080u;
+  w[1] = ((c[1] >> 6) | (c[2] << 20)) ^ 0x80808080u;
+  w[2] = ((c[2] >> 12) | (c[3] << 14)) ^ 0x80808080u;
+  w[3] = ((c[3] >> 18) | (c[4] << 8)) ^ 0x80808080u;
+  w[4] = c[4] >> 24;
+}
+
 enum { DOM_ELEMS = 0, DOM_MERGE = 1, DOM_MANY = 2, DOM_INT = 3 };
 
 static inline void limbs26(fe a, uint32_t l[5]) {

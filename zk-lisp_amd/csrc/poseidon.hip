@@ -92,6 +92,16 @@ HasherMont make_hasher_mont(const HasherConsts& h) {
       for (int k = 0; k < 12; k++) limbs26(fe_mul(h.mds[i * 12 + k], w), m.mdsl[i][k][u]);
   for (int r = 0; r < 27; r++)
     for (int i = 0; i < 12; i++) mont130(h.rc[r * 12 + i], m.rc130[r][i]);
+  {
+    uint32_t c[5];
+    const uint32_t z[5] = {0, 0, 0, 0, 0};
+    mont_cube130(z, c);
+    pm_pack_words(c, m.pmk0);
+    for (int t = 0; t < 2; t++) {
+      mont_cube130(m.dom130[t], c);
+      pm_pack_words(c, m.pmkt[t]);
+    }
+  }
   return m;
 }
 
@@ -569,10 +579,15 @@ __global__ __launch_bounds__(64 * TOP_WAVES) void merkle_top_kernel(fe* nodes, s
 }
 
 void launch_merkle(fe* d_nodes, size_t n, hipStream_t s, fe* d_coin, fe* d_root_out, int coin_mode) {
+  // the transcript step of coin_mode runs only in the launch that reaches the root: a tree that
+  // never gets there (fewer than two leaves) would silently leave the coin unseeded
+  if (coin_mode && n < 2) throw std::logic_error("launch_merkle: coin step requested on a tree without a root launch");
+  bool reached = false;
   for (size_t lvl = n / 2; lvl >= 1;) {
     if (lvl <= PW_MAX_ITEMS) {
       const size_t cnt = std::min<size_t>(lvl, TOP_SLOTS);
       const bool last = lvl / (cnt * 2) == 0;  // this launch reaches the root
+      reached |= last;
       merkle_top_kernel<<<(unsigned)(lvl / cnt), 64 * TOP_WAVES, 0, s>>>(d_nodes, lvl, (int)cnt, d_coin, d_root_out,
                                                                           last ? coin_mode : 0);
       lvl /= cnt * 2;
@@ -586,6 +601,7 @@ void launch_merkle(fe* d_nodes, size_t n, hipStream_t s, fe* d_coin, fe* d_root_
       merkle_level_kernel<<<pg_blocks(lvl), 256, 0, s>>>(d_nodes, lvl);
     lvl /= 2;
   }
+  if (coin_mode && !reached) throw std::logic_error("launch_merkle: no launch reached the root; coin step dropped");
 }
 
 __global__ PG_KERNEL void pg_permute_kernel(fe* st, size_t n) {

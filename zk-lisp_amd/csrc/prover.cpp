@@ -5,6 +5,7 @@
 // multiproof index sets and serialises Proof::to_bytes().
 #include <hip/hip_runtime.h>
 #include <malloc.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <atomic>
@@ -60,6 +61,22 @@ struct DBuf {
   ~DBuf() { if (p) (void)hipFree(p); }
 };
 
+// Process-wide account of the pinned host memory the library holds (zkl_hip_pinned_bytes):
+// every hipHostMalloc / hipHostFree of the library goes through these two.
+std::atomic<uint64_t> g_pin_cur{0}, g_pin_peak{0};
+void pin_alloc(void** p, size_t b) {
+  HIPCHECK(hipHostMalloc(p, b, hipHostMallocDefault));
+  const uint64_t c = g_pin_cur.fetch_add(b) + b;
+  uint64_t pk = g_pin_peak.load();
+  while (c > pk && !g_pin_peak.compare_exchange_weak(pk, c)) {
+  }
+}
+hipError_t pin_free(void* p, size_t b) {
+  if (!p) return hipSuccess;
+  g_pin_cur.fetch_sub(b);
+  return hipHostFree(p);
+}
+
 // Pinned host staging: copies from/to it are asynchronous DMA that neither blocks the host
 // until the stream drains nor goes through the runtime's pageable bounce buffers.
 struct HBuf {
@@ -67,16 +84,20 @@ struct HBuf {
   size_t bytes = 0;
   void ensure(size_t b) {
     if (b <= bytes) return;
-    if (p) (void)hipHostFree(p);
+    (void)release();
+    b += b / 4;  // sizes vary a little from proof to proof (query count, assertions)
+    pin_alloc(&p, b);
+    bytes = b;
+  }
+  hipError_t release() {
+    const hipError_t e = pin_free(p, bytes);
     p = nullptr;
     bytes = 0;
-    b += b / 4;  // sizes vary a little from proof to proof (query count, assertions)
-    HIPCHECK(hipHostMalloc(&p, b, hipHostMallocDefault));
-    bytes = b;
+    return e;
   }
   template <class T>
   T* at(size_t off = 0) const { return (T*)((char*)p + off); }
-  ~HBuf() { if (p) (void)hipHostFree(p); }
+  ~HBuf() { (void)release(); }
 };
 
 }  // namespace
@@ -381,7 +402,7 @@ void upload_trace_chunked(zkl_ctx* C, const void* h_trace, uint32_t W, size_t n,
     C->up_slot.assign(UP_SLOTS, nullptr);
     C->up_ev.assign(UP_SLOTS, nullptr);
     for (int k = 0; k < UP_SLOTS; k++) {
-      HIPCHECK(hipHostMalloc(&C->up_slot[k], UP_SLOT_BYTES, hipHostMallocDefault));
+      pin_alloc(&C->up_slot[k], UP_SLOT_BYTES);
       HIPCHECK(hipEventCreateWithFlags(&C->up_ev[k], hipEventDisableTiming));
     }
     C->up_slot_bytes = UP_SLOT_BYTES;
@@ -843,7 +864,12 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   uint32_t batch = 1u << std::min<uint32_t>(std::max<uint32_t>(o.grinding_factor, 14), 22);
   // test-only: ZKL_TEST_GRIND_FIRST=<tries> shrinks the first window, so a test reaches the host
   // continuation below (a path real proofs take with probability e^-8) and checks its nonce
-  if (const char* e = getenv("ZKL_TEST_GRIND_FIRST")) batch = (uint32_t)std::max(1L, std::min(atol(e), 1L << 22));
+  // (read per proof because a test process sets it per test; announced once per process)
+  if (const char* e = getenv("ZKL_TEST_GRIND_FIRST")) {
+    batch = (uint32_t)std::max(1L, std::min(atol(e), 1L << 22));
+    static std::once_flag said;
+    std::call_once(said, [&] { fprintf(stderr, "zkl_hip: test hook ZKL_TEST_GRIND_FIRST=%s active\n", e); });
+  }
   uint64_t base = 1;
   auto queue_windows = [&](const fe* d_seed, fe h_seed) {
     *hbest = o.grinding_factor == 0 ? 1ull : ~0ull;
@@ -917,7 +943,12 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   }
   for (size_t k = 0; k < nq; k++)
     for (int j = 0; j < Cc; j++) *ap++ = (uint64_t)(uintptr_t)(C->clde.f() + (size_t)j * N + pos[k]);
+  // every section checks its room before it writes (the bound above is an estimate of the plans)
+  auto room = [&](size_t k) {
+    if ((size_t)(ap - abase) + k > na_max) throw std::runtime_error("internal: gather plan bound");
+  };
   auto append_nodes = [&](const fe* tree, const Plan& plan) {
+    room(plan.node.size());
     for (uint64_t ix : plan.node) *ap++ = (uint64_t)(uintptr_t)(tree + ix);
   };
   Plan& tplan = C->tplan_s;
@@ -939,13 +970,13 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
         const size_t y = x & (h - 1);
         if (std::find(f.begin(), f.end(), y) == f.end()) f.push_back(y);
       }
+      room(2 * f.size());
       for (size_t y : f) { *ap++ = (uint64_t)(uintptr_t)(layer_ev(d) + y); *ap++ = (uint64_t)(uintptr_t)(layer_ev(d) + y + h); }
       batch_plan_into(h, f.data(), f.size(), fplan[d]);
       append_nodes(C->fri_tree.f() + tr_off[d], fplan[d]);
       dsz = h;
     }
   }
-  if ((size_t)(ap - abase) > na_max) throw std::runtime_error("internal: gather plan bound");
   HT("q_planned");
   const size_t na_g = (size_t)(ap - abase);
   C->gaddr.ensure((na_g + na_g / 4) * 8);
@@ -1152,14 +1183,18 @@ int zkl_hip_trace_buffer(zkl_ctx* c, uint32_t slot, size_t bytes, zkl_f128** out
     HIPCHECK(hipSetDevice(c->device));
     HBuf& b = c->tbuf[slot];
     if (bytes > b.bytes) {  // exact size: one segment shape is the common case
-      if (b.p) HIPCHECK(hipHostFree(b.p));
-      b.p = nullptr;
-      b.bytes = 0;
-      HIPCHECK(hipHostMalloc(&b.p, bytes, hipHostMallocDefault));
+      HIPCHECK(b.release());
+      pin_alloc(&b.p, bytes);
       b.bytes = bytes;
     }
     *out = (zkl_f128*)b.p;
   });
+}
+
+int zkl_hip_pinned_bytes(uint64_t* current, uint64_t* peak) {
+  if (current) *current = g_pin_cur.load();
+  if (peak) *peak = g_pin_peak.load();
+  return ZKL_OK;
 }
 
 void zkl_hip_destroy(zkl_ctx* c) {
@@ -1172,7 +1207,7 @@ void zkl_hip_destroy(zkl_ctx* c) {
   if (c->up) {
     (void)hipStreamSynchronize(c->up);
     (void)hipStreamDestroy(c->up);
-    for (void* p : c->up_slot) (void)hipHostFree(p);
+    for (void* p : c->up_slot) (void)pin_free(p, c->up_slot_bytes);
     for (hipEvent_t e : c->up_ev) (void)hipEventDestroy(e);
   }
   if (c->aux) {

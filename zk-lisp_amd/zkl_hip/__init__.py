@@ -169,6 +169,8 @@ def load_library():
                                       C.c_void_p, C.c_void_p]
     lib.zkl_hip_process_tuning.argtypes = [C.c_uint32, P(C.c_uint32)]
     lib.zkl_hip_trace_buffer.argtypes = [C.c_void_p, C.c_uint32, C.c_size_t, P(C.c_void_p)]
+    if hasattr(lib, "zkl_hip_pinned_bytes"):  # (older builds, loaded by tools/ for A/B, lack it)
+        lib.zkl_hip_pinned_bytes.argtypes = [P(C.c_uint64), P(C.c_uint64)]
     lib.zkl_program_new.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p,
                                     C.c_uint32, P(F128), P(C.c_void_p), P(C.c_uint32), P(C.c_uint32)]
     lib.zkl_build_segment_trace.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, P(AirPublicInputs),
@@ -462,7 +464,10 @@ def children_root(suite_id: bytes, digests, root_traces) -> bytes:
     zl1 root_trace) pairs of the children."""
     lib = load_library()
     out = (C.c_uint8 * 32)()
-    rc = lib.zkl_children_root(bytes(suite_id), b"".join(digests), b"".join(root_traces), len(digests), out)
+    digests, root_traces = [bytes(d) for d in digests], [bytes(r) for r in root_traces]
+    if len(digests) != len(root_traces) or any(len(x) != 32 for x in digests + root_traces):
+        raise ValueError("children_root: one 32-byte digest and one 32-byte root_trace per child")
+    rc = lib.zkl_children_root(_id32("suite_id", suite_id), b"".join(digests), b"".join(root_traces), len(digests), out)
     if rc:
         raise ZklError(rc, lib.zkl_hip_last_error(None).decode())
     return bytes(out)
@@ -805,6 +810,24 @@ def _vm_args(main_args):
     return out
 
 
+def pinned_bytes():
+    """(current, peak) bytes of pinned host memory the library holds (zkl_hip_pinned_bytes)."""
+    lib = load_library()
+    cur, peak = C.c_uint64(), C.c_uint64()
+    if not hasattr(lib, "zkl_hip_pinned_bytes"):
+        return 0, 0
+    lib.zkl_hip_pinned_bytes(C.byref(cur), C.byref(peak))
+    return cur.value, peak.value
+
+
+def _id32(name: str, v) -> bytes:
+    """A 32-byte program id / commitment argument: the C side reads exactly 32 bytes."""
+    b = bytes(v)
+    if len(b) != 32:
+        raise ValueError(f"{name} must be 32 bytes, got {len(b)}")
+    return b
+
+
 def build_trace(ops, program_id: bytes, program_commitment: bytes | None = None, secret_args=(), main_args=(),
                 rom0: int = 0):
     """build_full_trace (vm/trace/mod.rs:434-524) of an op list through zkl_build_trace:
@@ -812,13 +835,14 @@ def build_trace(ops, program_id: bytes, program_commitment: bytes | None = None,
     ops' features.  program_commitment defaults to program_id (the AIR binds pi_prog at row 0 to
     the commitment, air/mod.rs)."""
     lib = load_library()
+    program_id = _id32("program_id", program_id)
+    commit = _id32("program_commitment", program_commitment if program_commitment is not None else program_id)
     arr = (ZklOp * len(ops))(*ops)
-    commit = bytes(program_commitment if program_commitment is not None else program_id)
     sec = (C.c_uint64 * max(1, len(secret_args)))(*secret_args)
     ma = _vm_args(list(main_args))
     r0 = F128(rom0 & (2 ** 64 - 1), rom0 >> 64)
     w, n = C.c_uint32(), C.c_uint32()
-    args = (C.cast(arr, C.c_void_p), len(ops), bytes(program_id), commit, C.cast(sec, C.c_void_p), len(secret_args),
+    args = (C.cast(arr, C.c_void_p), len(ops), program_id, commit, C.cast(sec, C.c_void_p), len(secret_args),
             C.cast(ma, C.c_void_p), len(main_args), C.byref(r0))
     rc = lib.zkl_build_trace(*args, None, None, C.byref(w), C.byref(n))
     if rc != 0:
@@ -836,7 +860,7 @@ def rom_acc_from_program(ops, program_id: bytes):
     lib = load_library()
     arr = (ZklOp * len(ops))(*ops)
     out = (F128 * 3)()
-    rc = lib.zkl_rom_acc_from_program(C.cast(arr, C.c_void_p), len(ops), bytes(program_id), out)
+    rc = lib.zkl_rom_acc_from_program(C.cast(arr, C.c_void_p), len(ops), _id32("program_id", program_id), out)
     if rc != 0:
         raise ZklError(rc, "rom_acc_from_program: invalid program")
     return [e.lo | (e.hi << 64) for e in out]
@@ -884,14 +908,15 @@ class Program:
     def __init__(self, ops, program_id: bytes, program_commitment: bytes | None = None, secret_args=(),
                  main_args=(), rom0: int = 0):
         self.lib = load_library()
+        program_id = _id32("program_id", program_id)
+        commit = _id32("program_commitment", program_commitment if program_commitment is not None else program_id)
         arr = (ZklOp * len(ops))(*ops)
-        commit = bytes(program_commitment if program_commitment is not None else program_id)
         sec = (C.c_uint64 * max(1, len(secret_args)))(*secret_args)
         ma = _vm_args(list(main_args))
         r0 = F128(rom0 & (2 ** 64 - 1), rom0 >> 64)
         w, n = C.c_uint32(), C.c_uint32()
         self.ptr = C.c_void_p()
-        rc = self.lib.zkl_program_new(C.cast(arr, C.c_void_p), len(ops), bytes(program_id), commit,
+        rc = self.lib.zkl_program_new(C.cast(arr, C.c_void_p), len(ops), program_id, commit,
                                       C.cast(sec, C.c_void_p), len(secret_args), C.cast(ma, C.c_void_p),
                                       len(main_args), C.byref(r0), C.byref(self.ptr), C.byref(w), C.byref(n))
         if rc != 0:
