@@ -206,6 +206,25 @@ __host__ __device__ inline void mul_acc(fe a, fe b, uint32_t acc[9]) {
   acc[8] += (uint32_t)c;
 }
 
+// acc[0..9) += v (lazy sum of field elements, no multiplication; <= 2^32 terms)
+__host__ __device__ inline void add_acc(fe v, uint32_t acc[9]) {
+  const uint32_t w[4] = {(uint32_t)v.lo, (uint32_t)(v.lo >> 32), (uint32_t)v.hi, (uint32_t)(v.hi >> 32)};
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint64_t t = (uint64_t)acc[i] + w[i] + c;
+    acc[i] = (uint32_t)t;
+    c = t >> 32;
+  }
+#pragma unroll
+  for (int i = 4; i < 8; i++) {
+    uint64_t t = (uint64_t)acc[i] + c;
+    acc[i] = (uint32_t)t;
+    c = t >> 32;
+  }
+  acc[8] += (uint32_t)c;
+}
+
 // ---------------------------------------------------------------- host multiply
 typedef unsigned __int128 u128;
 inline u128 to128(fe a) { return ((u128)a.hi << 64) | a.lo; }

@@ -78,8 +78,9 @@ void upload_air_consts(ProofConsts* dK, const AirDevice& a, hipStream_t s);
 // transition composition coefficients alpha_j: copied device->device from the draw buffer
 void upload_alphas_from_device(ProofConsts* dK, const fe* d_alphas, int n, hipStream_t s);
 // dK->pose_k from dK->alpha and the AIR's round constants (after upload_alphas_from_device; the
-// Poseidon block's alphas come first in the evaluation order)
-void launch_pose_k(const ProofConsts* dK, DerivedConsts* dD, hipStream_t s);
+// Poseidon block's alphas come first in the evaluation order), and the prefix sums dD->apre of
+// the first n_tc alphas (the constraint groups of air_eval.h)
+void launch_pose_k(const ProofConsts* dK, DerivedConsts* dD, int n_tc, bool pose, hipStream_t s);
 // The DEEP coefficients straight from the draw buffer (no host round trip): dD->deep,
 // dD->deep_m (limbs of g * 2^156) and dD->deep_sz from the OOD frame d_frame (t(z) [W] | H(z) [C]
 // | t(zg) [W] | H(zg) [C]).  n = W + C <= 256.
@@ -198,6 +199,7 @@ struct ProofConsts {
 // kept apart from ProofConsts, which only host/device copies write.
 struct DerivedConsts {
   fe pose_k[27];            // sum_i alpha_{12j+i} rc[j][i] per Poseidon round (launch_pose_k)
+  fe apre[1025];            // alpha prefix sums: apre[i] = alpha_0 + .. + alpha_(i-1) (launch_pose_k)
   fe deep[512];             // DEEP coefficients (trace then composition columns)
   uint32_t deep_m[512][5];  // the same as 26-bit limbs of g * 2^156 mod p (deep_kernel)
   fe deep_sz[2];            // sum_i g_i * frame_i(z), sum_i g_i * frame_i(z g) (deep_coeffs_kernel)

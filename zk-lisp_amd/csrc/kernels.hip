@@ -31,14 +31,31 @@ void upload_alphas_from_device(ProofConsts* dK, const fe* d, int n, hipStream_t 
   if (n > 1024) throw std::invalid_argument("more than 1024 transition constraints");
   ZKL_HIPCHECK(hipMemcpyAsync(dK->alpha, d, sizeof(fe) * n, hipMemcpyDeviceToDevice, s));
 }
-__global__ void pose_k_kernel(const ProofConsts* K, DerivedConsts* D) {
+// one workgroup of 1024 threads: the Poseidon round constants' alpha sums (when the layout has the
+// block) and the inclusive scan of the n_tc alphas in LDS (Hillis-Steele, 10 steps)
+__global__ __launch_bounds__(1024) void pose_k_kernel(const ProofConsts* K, DerivedConsts* D, int n_tc, int pose) {
   const int j = (int)threadIdx.x;
-  if (j >= 27) return;
-  uint32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (int i = 0; i < 12; i++) mul_acc(K->alpha[12 * j + i], K->air.pose_rc[j][i], acc);
-  D->pose_k[j] = reduce288(acc);
+  if (pose && j < 27) {
+    uint32_t acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 12; i++) mul_acc(K->alpha[12 * j + i], K->air.pose_rc[j][i], acc);
+    D->pose_k[j] = reduce288(acc);
+  }
+  __shared__ fe sc[1024];
+  sc[j] = j < n_tc ? K->alpha[j] : fe_zero();
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const fe add = j >= d ? sc[j - d] : fe_zero();
+    __syncthreads();
+    sc[j] = fe_add(sc[j], add);
+    __syncthreads();
+  }
+  D->apre[j + 1] = sc[j];
+  if (j == 0) D->apre[0] = fe_zero();
 }
-void launch_pose_k(const ProofConsts* dK, DerivedConsts* dD, hipStream_t s) { pose_k_kernel<<<1, 64, 0, s>>>(dK, dD); }
+void launch_pose_k(const ProofConsts* dK, DerivedConsts* dD, int n_tc, bool pose, hipStream_t s) {
+  if (n_tc < 0 || n_tc > 1024) throw std::invalid_argument("launch_pose_k: more than 1024 transition constraints");
+  pose_k_kernel<<<1, 1024, 0, s>>>(dK, dD, n_tc, pose ? 1 : 0);
+}
 
 // =====================================================================================
 // NTT: in-place radix-2 passes, up to 8 stages per pass staged through LDS.
@@ -741,7 +758,7 @@ __device__ __forceinline__ void constraint_eval_body(const fe* __restrict__ lde,
   const size_t per_period = ce / (c_ce.n / 32);
   const fe* per = pertab + (i % per_period) * 31;
   if (PART == 1) {
-    out[i] = air_transition_sum<POSE, RM, 1>(c_air, cur, nxt, per, fe_zero(), K->alpha, D->pose_k);
+    out[i] = air_transition_sum<POSE, RM, 1>(c_air, cur, nxt, per, fe_zero(), K->alpha, D->pose_k, D->apre);
     return;
   }
   const size_t blow = ce / c_ce.n;
@@ -750,7 +767,7 @@ __device__ __forceinline__ void constraint_eval_body(const fe* __restrict__ lde,
   fe x_gl = fe_sub_sel(x, c_ce.gl);
   fe xn_m1 = c_ce.xn_m1[i % blow];
   fe p_last = fe_mul(fe_mul(c_ce.lagr, xn_m1), xinv[i]);  // xinv[i] = 1 / (x - g^(n-1))
-  fe tsum = air_transition_sum<POSE, RM, PART>(c_air, cur, nxt, per, p_last, K->alpha, D->pose_k);
+  fe tsum = air_transition_sum<POSE, RM, PART>(c_air, cur, nxt, per, p_last, K->alpha, D->pose_k, D->apre);
   if (PART == 2) tsum = fe_add(tsum, pose_part[i]);
   // boundary: sum_c P_c(x) M_c(x) - W(x)
   uint32_t bacc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};

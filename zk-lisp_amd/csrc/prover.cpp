@@ -617,7 +617,7 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
   check_launch("composition coefficient draws");
   coin.counter += ndraw;
   upload_alphas_from_device(dK, C->draws.f(), air.n_tc, s);
-  if (air.dev.pose_block) launch_pose_k(dK, dD, s);
+  launch_pose_k(dK, dD, air.n_tc, air.dev.pose_block != 0, s);
 
   HIPCHECK(hipMemsetAsync(C->bvec.p, 0, (size_t)(nb + 1) * n * sizeof(fe), s));
   const fe* betas = C->draws.f() + air.n_tc;
