@@ -386,6 +386,150 @@ __global__ __launch_bounds__(THREADS) void ntt_dit_lazy_kernel(fe* __restrict__ 
   }
 }
 
+// Natural -> bit-reversed transforms (the iNTTs and the forward DIF passes) with the DIT kernel's
+// lazy limbs: Cooley-Tukey butterflies y0 = x0 + x1 w, y1 = x0 - x1 w (+Q) in decreasing-stride
+// order, where the twiddle of a stage depends only on the butterfly's block: at global half size H
+// (m = N / 2H blocks) block b takes w_(2m)^brv(b) (entry m + brv_(log m)(b) of the stage-major
+// table), and the result equals the Gentleman-Sande DIF output exactly (round 6; the canonical DIF
+// kernel reduced every sum, and its a + b chains cannot stay lazy).  Same pass split, element
+// mapping, src / scale conventions and two-stages-per-LDS-round-trip quads as the kernels above.
+template <int ELEMS, int THREADS>
+__global__ __launch_bounds__(THREADS) void ntt_ct_lazy_kernel(fe* __restrict__ data, size_t ncols, int logN, int r,
+                                                                 int logS, MontTab roots, const fe* __restrict__ src,
+                                                                 int src_logb, const fe* __restrict__ scale) {
+  constexpr int PITCHED = ELEMS + ELEMS / 16;
+  __shared__ uint4 bufA[PITCHED];
+  __shared__ uint32_t bufB[PITCHED];
+  const int R = 1 << r;
+  const int G = ELEMS >> r;
+  const size_t S = (size_t)1 << logS;
+  const int log_gpc = logN - r;
+  const size_t gpc = (size_t)1 << log_gpc;
+  const bool gfast = S >= (size_t)G;
+  const int pitch = R >= 16 ? R + 1 : R;
+  size_t col_fixed = 0, qbase = 0;
+  const bool whole = gpc >= (size_t)G;
+  if (whole) {
+    col_fixed = blockIdx.x % (unsigned)ncols;
+    qbase = (size_t)(blockIdx.x / (unsigned)ncols) * G;
+  }
+  auto locate = [&](int g, size_t& col, size_t& q) -> bool {
+    if (whole) {
+      col = col_fixed;
+      q = qbase + g;
+      return true;
+    }
+    const size_t qg = (size_t)blockIdx.x * G + g;
+    col = qg >> log_gpc;
+    q = qg & (gpc - 1);
+    return col < ncols;
+  };
+  auto addr = [&](int g, int t, bool& ok) -> size_t {
+    size_t col, q;
+    ok = locate(g, col, q);
+    const size_t L = q & (S - 1), Hb = q >> logS;
+    return (col << logN) + ((Hb << logS) << r) + (size_t)t * S + L;
+  };
+  const size_t Nmask = ((size_t)1 << logN) - 1;
+  for (int e = threadIdx.x; e < ELEMS; e += THREADS) {
+    const int g = gfast ? (e % G) : (e >> r);
+    const int t = gfast ? (e / G) : (e & (R - 1));
+    bool ok;
+    const size_t a = addr(g, t, ok);
+    fe v = fe_zero();
+    if (ok) v = src ? src[((a >> logN) << (logN - src_logb)) + ((a & Nmask) >> src_logb)] : data[a];
+    uint32_t l[5];
+    to26(v, l);
+    bufA[g * pitch + t] = make_uint4(l[0], l[1], l[2], l[3]);
+    bufB[g * pitch + t] = l[4];
+  }
+  __syncthreads();
+  auto ld = [&](int o, uint32_t x[5]) {
+    const uint4 a = bufA[o];
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = bufB[o];
+  };
+  auto st = [&](int o, const uint32_t x[5]) {
+    bufA[o] = make_uint4(x[0], x[1], x[2], x[3]);
+    bufB[o] = x[4];
+  };
+  // twiddle of block b at local stage lh of group q: w_(2m)^brv(b), m = N / 2H, H = 2^lh S
+  auto tw = [&](int lh, size_t q, int t0, uint32_t wm[5]) {
+    const int logm = logN - 1 - lh - logS;
+    const size_t b = (q >> logS) * ((size_t)R >> (lh + 1)) + (size_t)(t0 >> (lh + 1));
+    const size_t e = ((size_t)1 << logm) + (logm ? (size_t)(__brevll((unsigned long long)b) >> (64 - logm)) : 0);
+    const uint4 q4 = roots.l4[e];
+    wm[0] = q4.x; wm[1] = q4.y; wm[2] = q4.z; wm[3] = q4.w; wm[4] = roots.l1[e];
+  };
+  auto bfly = [&](uint32_t x0[5], uint32_t x1[5], const uint32_t wm[5]) {
+    uint32_t v[5];
+    mont_mul(x1, wm, v);
+#pragma unroll
+    for (int l = 0; l < 5; l++) {
+      x1[l] = x0[l] + NTT_Q[l] - v[l];
+      x0[l] = x0[l] + v[l];
+    }
+  };
+  int lh = r - 1;
+  // two stages per LDS round trip: a thread takes the quad t0, t0+hl, t0+2hl, t0+3hl (hl = 2^(lh-1));
+  // stage lh pairs (0,2), (1,3) under one twiddle, stage lh-1 pairs (0,1) and (2,3)
+  for (; lh >= 1; lh -= 2) {
+    const int hl = 1 << (lh - 1);
+    constexpr int QPT = ELEMS / 4 / THREADS;
+#pragma unroll
+    for (int i = 0; i < QPT; i++) {
+      const int u = threadIdx.x + THREADS * i;
+      const int g = u % G;
+      const int w = u / G;
+      const int k = w & (hl - 1);
+      const int t0 = ((w >> (lh - 1)) << (lh + 1)) + k;
+      size_t colx, q;
+      locate(g, colx, q);
+      const int o = g * pitch + t0;
+      uint32_t a0[5], a1[5], a2[5], a3[5], w1[5], w2[5], w3[5];
+      ld(o, a0); ld(o + hl, a1); ld(o + 2 * hl, a2); ld(o + 3 * hl, a3);
+      tw(lh, q, t0, w1);
+      tw(lh - 1, q, t0, w2);
+      tw(lh - 1, q, t0 + 2 * hl, w3);
+      bfly(a0, a2, w1);
+      bfly(a1, a3, w1);
+      bfly(a0, a1, w2);
+      bfly(a2, a3, w3);
+      st(o, a0); st(o + hl, a1); st(o + 2 * hl, a2); st(o + 3 * hl, a3);
+    }
+    __syncthreads();
+  }
+  if (lh == 0) {  // odd stage count: the last radix-2 stage
+    constexpr int BPT = ELEMS / 2 / THREADS;
+#pragma unroll
+    for (int i = 0; i < BPT; i++) {
+      const int u = threadIdx.x + THREADS * i;
+      const int g = u % G;
+      const int t0 = (u / G) << 1;
+      size_t colx, q;
+      locate(g, colx, q);
+      const int o = g * pitch + t0;
+      uint32_t x0[5], x1[5], wm[5];
+      ld(o, x0); ld(o + 1, x1);
+      tw(0, q, t0, wm);
+      bfly(x0, x1, wm);
+      st(o, x0); st(o + 1, x1);
+    }
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < ELEMS; e += THREADS) {
+    const int g = gfast ? (e % G) : (e >> r);
+    const int t = gfast ? (e / G) : (e & (R - 1));
+    bool ok;
+    const size_t a = addr(g, t, ok);
+    const uint4 a4 = bufA[g * pitch + t];
+    const uint32_t l[5] = {a4.x, a4.y, a4.z, a4.w, bufB[g * pitch + t]};
+    if (ok) {
+      const fe v = ntt_canon(l);
+      data[a] = scale ? fe_mul(v, scale[bitrev((uint32_t)(a & Nmask), logN)]) : v;
+    }
+  }
+}
+
 // 8-stage DIT pass held in registers: 2048 elements (8 groups of 256 at consecutive L, whole
 // 128-byte lines) on 256 threads, 8 elements per thread.  Stages 0-2 run on the elements a
 // thread loads straight from HBM (t = 8j + u), stages 3-5 and 6-7 after one LDS exchange each
@@ -555,6 +699,16 @@ static int ntt8_lfast(int logS) {
   return m == 1 || (m == 2 && logS >= 11) ? 1 : 0;
 }
 
+// natural -> bit-reversed passes in the lazy Cooley-Tukey form (default) or the canonical DIF
+// kernel (ZKL_NTT_CT=0, A/B); both give the same output
+static bool ntt_ct_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("ZKL_NTT_CT");
+    return !(e && !strcmp(e, "0"));
+  }();
+  return on;
+}
+
 static int ilog2s(size_t n) { int k = 0; while (((size_t)1 << k) < n) k++; return k; }
 
 // Stage split of one transform into LDS passes.  The pass over the largest stride S (the
@@ -613,8 +767,24 @@ static void ntt_passes(fe* d, size_t ncols, size_t N, bool dif, int lo, int hi, 
       int logS = cur - r + 1;
       size_t groups = (N >> r) * ncols;
       size_t G = NTT_ELEMS >> r;
-      ntt_pass_kernel<true><<<(unsigned)((groups + G - 1) / G), NTT_THREADS, 0, s>>>(
-          d, ncols, logN, r, logS, roots, logTab, k + 1 == rs.size() ? src : nullptr, 0, k == 0 ? scale : nullptr);
+      const fe* sp = k + 1 == rs.size() ? src : nullptr;
+      const fe* sc = k == 0 ? scale : nullptr;
+      if (ntt_lazy_enabled() && ntt_ct_enabled()) {
+        // lazy Cooley-Tukey passes (ntt_ct_lazy_kernel); half-line groups take the wide form
+        const int wm = ntt_wide_mode();
+        const bool wide = wm > 0 && G < 8 && ((size_t)1 << logS) >= G;
+        const size_t Gw = wide ? 2 * G : G;
+        const unsigned grid = (unsigned)((groups + Gw - 1) / Gw);
+        if (wide && wm == 2)
+          ntt_ct_lazy_kernel<2 * NTT_ELEMS, 2 * NTT_THREADS><<<grid, 2 * NTT_THREADS, 0, s>>>(d, ncols, logN, r, logS, roots, sp, 0, sc);
+        else if (wide)
+          ntt_ct_lazy_kernel<2 * NTT_ELEMS, NTT_THREADS><<<grid, NTT_THREADS, 0, s>>>(d, ncols, logN, r, logS, roots, sp, 0, sc);
+        else
+          ntt_ct_lazy_kernel<NTT_ELEMS, NTT_THREADS><<<grid, NTT_THREADS, 0, s>>>(d, ncols, logN, r, logS, roots, sp, 0, sc);
+      } else {
+        ntt_pass_kernel<true><<<(unsigned)((groups + G - 1) / G), NTT_THREADS, 0, s>>>(d, ncols, logN, r, logS, roots,
+                                                                                      logTab, sp, 0, sc);
+      }
       cur -= r;
     }
   } else {

@@ -538,6 +538,9 @@ void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np
 // lvl/cnt, with a workgroup barrier between levels; waves without a live node skip the
 // permutation.  A launch per level would add ~10 us of dispatch latency to each of these
 // permutation-latency-bound levels.
+#ifndef TOP_LDS_CFG
+#define TOP_LDS_CFG 1
+#endif
 constexpr int TOP_WAVES = 8 / PW_PER_WAVE;
 constexpr int TOP_SLOTS = TOP_WAVES * PW_PER_WAVE;  // 8
 // coin_mode (the launch that reaches the root, one workgroup): after the root, wave 0 runs the
@@ -547,23 +550,33 @@ constexpr int TOP_SLOTS = TOP_WAVES * PW_PER_WAVE;  // 8
 __global__ __launch_bounds__(64 * TOP_WAVES) void merkle_top_kernel(fe* nodes, size_t lvl, int cnt, fe* coin,
                                                                     fe* root_out, int coin_mode) {
   __shared__ __align__(16) uint32_t pw_lds[TOP_WAVES * PW_WAVE_WORDS];
+  // the level just computed, also kept in LDS (double-buffered): the next level takes its children
+  // from here instead of a global store / barrier / load round trip (round 6)
+  __shared__ fe tn[2][TOP_SLOTS];
   PWGroup P;
   pw_init(P, pw_lds);
   const int wave_slot0 = (int)(threadIdx.x >> 6) * PW_PER_WAVE;
   const int slot = wave_slot0 + P.g;
   size_t L = lvl, base = (size_t)blockIdx.x * cnt;
-  for (int c = cnt; c >= 1; c >>= 1, L >>= 1, base >>= 1) {
+  int par = 0;
+  for (int c = cnt; c >= 1; c >>= 1, L >>= 1, base >>= 1, par ^= 1) {
     if (wave_slot0 < c) {  // wave-uniform
       const bool live = P.g < PW_PER_WAVE && slot < c;
       const size_t i = L + base + (live ? slot : 0);
-      fe d = pw_sponge<DOM_MERGE>(P, live, 2, [&](int j) { return nodes[2 * i + j]; });
-      if (live && P.e == 0 && P.h == 0) nodes[i] = d;
+      const int sl = live ? slot : 0;
+      fe d = pw_sponge<DOM_MERGE>(P, live, 2, [&](int j) {
+        return (c == cnt || !TOP_LDS_CFG) ? nodes[2 * i + j] : tn[par ^ 1][2 * sl + j];
+      });
+      if (live && P.e == 0 && P.h == 0) {
+        nodes[i] = d;
+        tn[par][slot] = d;
+      }
     }
     __syncthreads();
   }
   if (coin_mode && threadIdx.x < 64) {  // wave 0 of the single workgroup
     const bool live = P.g == 0;
-    const fe seed = coin[0], r = nodes[1];
+    const fe seed = coin[0], r = TOP_LDS_CFG ? tn[par ^ 1][0] : nodes[1];
     fe s1 = pw_sponge<DOM_MERGE>(P, live, 2, [&](int j) { return j == 0 ? seed : r; });
     fe a = fe_zero();
     if (coin_mode == 2) {
