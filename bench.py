@@ -260,7 +260,7 @@ def valu_roofline(perms_per_s):
 
 def load_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed PMC summary of the newest round."""
-    for r in ("r05", "r04", "r03", "r02", "r01"):
+    for r in ("r06", "r05", "r04", "r03", "r02", "r01"):
         p = os.path.join(ROOT, "profiles", r, "pmc_traffic.json")
         try:
             d = json.load(open(p))

@@ -287,10 +287,29 @@ __host__ __device__ inline fe fe_pow64(fe b, uint64_t e) {
   }
   return r;
 }
-// Fermat inverse a^(p-2); zero -> zero
+// Fermat inverse a^(p-2); zero -> zero.  p - 2 = [80 ones][1101 0010][40 ones] in binary, so an
+// addition chain over a^(2^k - 1) takes 127 squarings and 12 multiplications instead of the 128 +
+// ~125 of square-and-multiply (round 6: the DEEP denominators' batch inversion, coset_inv_kernel).
+__host__ __device__ inline fe fe_sqr_n(fe a, int n) {
+  for (int i = 0; i < n; i++) a = fe_mul(a, a);
+  return a;
+}
 __host__ __device__ inline fe fe_inv(fe a) {
   if (fe_is_zero(a)) return a;
-  return fe_pow(a, P_LO - 2, P_HI);
+  const fe a1 = a;
+  const fe a2 = fe_mul(fe_sqr_n(a1, 1), a1);     // a^(2^2 - 1)
+  const fe a4 = fe_mul(fe_sqr_n(a2, 2), a2);
+  const fe a8 = fe_mul(fe_sqr_n(a4, 4), a4);
+  const fe a16 = fe_mul(fe_sqr_n(a8, 8), a8);
+  const fe a32 = fe_mul(fe_sqr_n(a16, 16), a16);
+  const fe a40 = fe_mul(fe_sqr_n(a32, 8), a8);
+  fe r = fe_mul(fe_sqr_n(a40, 40), a40);         // a^(2^80 - 1)
+  const uint32_t mid = 0xD2;                      // bits 47..40 of p - 2
+  for (int b = 7; b >= 0; b--) {
+    r = fe_mul(r, r);
+    if ((mid >> b) & 1) r = fe_mul(r, a1);
+  }
+  return fe_mul(fe_sqr_n(r, 40), a40);           // then 40 ones
 }
 
 // x * 2^64 mod p  (fold of the high half of a 32-byte sponge chunk, utils.rs:359-371)

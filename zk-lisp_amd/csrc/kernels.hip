@@ -1310,6 +1310,7 @@ namespace zkl {
 const char* kernels_build_config() {
   return "NTT_ELEMS=" ZKL_STR(NTT_ELEMS_CFG) ";NTT_THREADS=" ZKL_STR(NTT_THREADS_CFG) ";CE_WAVES=" ZKL_STR(
       CE_WAVES_CFG) ";CE_POSE_WAVES=" ZKL_STR(CE_POSE_WAVES_CFG) ";DEEP_PTS=" ZKL_STR(DEEP_PTS_CFG) ";DEEP_COLS=" ZKL_STR(
-      DEEP_COLS_CFG);
+      DEEP_COLS_CFG) ";CE_GROUPS=" ZKL_STR(CE_GROUPS_CFG) ";CE_DOT=" ZKL_STR(CE_DOT_CFG) ";CE_BRANCHFREE=" ZKL_STR(
+      CE_BRANCHFREE_CFG);
 }
 }  // namespace zkl

@@ -637,10 +637,23 @@ void launch_permute(fe* d_states, size_t n, int engine, hipStream_t s) {
     pg_permute_kernel<<<pg_blocks(n), 256, 0, s>>>(d_states, n);
 }
 
+// small draw batches (the query positions, the DEEP coefficients) are one permutation's latency:
+// the 48-lane form (~20 us) instead of the 12-lane one (~34 us, round 6 kernel trace)
+__global__ __launch_bounds__(256) void draw_wide_kernel(fe seed, const fe* seed_p, uint64_t base, size_t k, fe* out) {
+  if (seed_p) seed = *seed_p;
+  PW_SETUP();
+  const bool live = P.g < PW_PER_WAVE && item < k;
+  const uint64_t ctr = base + 1 + (live ? item : 0);
+  fe d = pw_sponge<DOM_INT>(P, live, 2, [&](int j) { return j == 0 ? seed : fe{ctr, 0}; });
+  if (live && P.e == 0 && P.h == 0) out[item] = d;
+}
+
 void launch_draws(fe seed, uint64_t base, size_t k, fe* d_out, hipStream_t s, const fe* d_seed) {
   if (!k) return;
   if (hash_engine() == 1 && k >= pm_min_items())
     PM_GO(draw_pm_kernel, k, false, s)(seed, d_seed, base, k, d_out);
+  else if (k <= PW_MAX_ITEMS)
+    draw_wide_kernel<<<pw_blocks(k), 256, 0, s>>>(seed, d_seed, base, k, d_out);
   else
     draw_kernel<<<pg_blocks(k), 256, 0, s>>>(seed, d_seed, base, k, d_out);
 }
@@ -757,6 +770,7 @@ const char* poseidon_build_config() {
   return "PM_WAVES=" ZKL_STR(PM_WAVES_CFG) ";PM_WIDE=" ZKL_STR(PM_WIDE_CFG) ";PM_ROW_WAVES=" ZKL_STR(
       PM_ROW_WAVES_CFG) ";PM_IGLP=" ZKL_STR(PM_IGLP_CFG) ";TAIL_PRIO=" ZKL_STR(TAIL_PRIO_CFG) ";PW_MAX_ITEMS=" ZKL_STR(
       PW_MAX_ITEMS_CFG) ";PM_ROW_BIG=" ZKL_STR(PM_ROW_BIG_CFG) ";POSEIDON_SCHED=" ZKL_STR(
-      ZKL_POSEIDON_SCHED_NAME);
+      ZKL_POSEIDON_SCHED_NAME) ";PM_PRUNE=" ZKL_STR(PM_PRUNE_CFG) ";PM_MFMA_PROBE=" ZKL_STR(PM_MFMA_PROBE_CFG)
+      ";TOP_LDS=" ZKL_STR(TOP_LDS_CFG);
 }
 }  // namespace zkl
