@@ -21,6 +21,8 @@ python3 -c "import json; d=json.load(open('$out/bench.json')); print(d['value'],
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o run --output-format csv -- python3 $root/bench.py --steps 5 --warmup 2 --no-cpu-baseline --c3-segments 0 --c5-log-n 0 --host-steps 0 --program-steps 0 --programs none > $out/prof_bench.json 2> $out/prof.err || { echo "rocprof rc=$?"; tail -5 $out/prof.err; exit 1; }
 cd $root
+python3 tools/ktrace_proof.py $(find $out/prof -name "*kernel_trace.csv" | head -1) > $out/proof_timeline.txt || exit 1
+tail -1 $out/proof_timeline.txt
 bash scripts/pmc_sq_rows.sh $tag/sq || exit 1
 bash scripts/pmc_quick.sh $tag/pmcq || exit 1
 echo done
