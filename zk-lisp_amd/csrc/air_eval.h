@@ -31,7 +31,7 @@ namespace zkl {
 #define AE_SUB fe_sub_sel
 #endif
 #ifndef CE_DOT_CFG
-#define CE_DOT_CFG 1
+#define CE_DOT_CFG 0
 #endif
 // CE_GROUPS_CFG: which groups are formed (A/B; 0 = one product per constraint): 1 VmCtrlAir
 // p_map / s_high, 2 g_carry / s_low, 4 p_final / s_write, 8 p_final / s_eq, 16 RomAir rounds
@@ -263,8 +263,10 @@ __host__ __device__ __forceinline__ fe air_transition_sum(const AirDevice& c_air
                use_div128 = m & (1u << 5), use_assert = m & 1u, use_abit = m & 2u, use_arange = m & 4u;
     fe pi2 = fe_sqr(pi), pi4 = fe_sqr(pi2), pi6 = fe_mul(pi4, pi2);
     fe s_write = fe_mul(s_low, pi6), s_eq = fe_mul(s_low, pi4);
-    // the selected operands are dot products of selector and register columns: lazy 288-bit sums
-    // and one reduction each (CE_DOT_CFG; 0 = one reduced product per term), two at a time
+    // the selected operands are dot products of selector and register columns.  CE_DOT_CFG = 1
+    // forms them as lazy 288-bit sums with one reduction each, two at a time: 0.5% faster on the
+    // headline evaluator but it reads the register columns three times (PMC fetch 3.16 -> 3.80 GB
+    // per launch, profiles/r06/final), so the default keeps one pass of reduced products.
     fe a_val, b_val, c_val, d0n, d0c, d1n;
     if (CE_DOT_CFG) {
       auto dot2 = [&](int sx, int sy, bool nx, bool ny, fe& vx, fe& vy) {

@@ -966,9 +966,19 @@ void prove_impl(zkl_ctx* C, const void* d_trace_in, bool trace_on_host, uint32_t
       const std::vector<size_t>& p = d ? fpos[d - 1] : pos;
       std::vector<size_t>& f = fpos[d];
       f.clear();
-      for (size_t x : p) {  // fold positions, first occurrence kept (FriProver::build_proof order)
+      // fold positions, first occurrence kept (FriProver::build_proof order); a 512-slot open
+      // addressing set instead of a linear search per position (nq <= 256)
+      uint64_t seen_key[512];
+      uint8_t seen[512] = {0};
+      for (size_t x : p) {
         const size_t y = x & (h - 1);
-        if (std::find(f.begin(), f.end(), y) == f.end()) f.push_back(y);
+        size_t k = (size_t)(((uint64_t)y * 0x9E3779B97F4A7C15ull) >> 55);
+        while (seen[k] && seen_key[k] != y) k = (k + 1) & 511;
+        if (!seen[k]) {
+          seen[k] = 1;
+          seen_key[k] = y;
+          f.push_back(y);
+        }
       }
       room(2 * f.size());
       for (size_t y : f) { *ap++ = (uint64_t)(uintptr_t)(layer_ev(d) + y); *ap++ = (uint64_t)(uintptr_t)(layer_ev(d) + y + h); }
