@@ -533,16 +533,23 @@ void launch_hash_rows(const fe* d_mat, uint32_t ncols, size_t nrows, uint32_t np
     hash_rows_kernel<0><<<pg_blocks(nrows), 256, 0, s>>>(d_mat, ncols, nrows, psize, merge, d_out, split);
 }
 
-// Tree top: several levels per launch.  Workgroup g (4 waves, 8 wide groups, one wave per
-// SIMD) owns nodes [cnt*g, cnt*g + cnt) of level lvl and reduces them to one node of level
+// Tree top: several levels per launch.  Workgroup g (TOP_WAVES waves, one 48-lane state each)
+// owns nodes [cnt*g, cnt*g + cnt) of level lvl and reduces them to one node of level
 // lvl/cnt, with a workgroup barrier between levels; waves without a live node skip the
 // permutation.  A launch per level would add ~10 us of dispatch latency to each of these
 // permutation-latency-bound levels.
 #ifndef TOP_LDS_CFG
 #define TOP_LDS_CFG 1
 #endif
-constexpr int TOP_WAVES = 8 / PW_PER_WAVE;
-constexpr int TOP_SLOTS = TOP_WAVES * PW_PER_WAVE;  // 8
+// waves per workgroup (one state each): 8 gives four levels per launch, the first at two waves
+// per SIMD; 4 gives three levels per launch, all but a tree's 2048-node level at one wave per SIMD
+// (round 6 A/B, profiles/r06/top_waves: Merkle family 10.87 -> 10.69 ms per proof)
+#ifndef TOP_WAVES_CFG
+#define TOP_WAVES_CFG 4
+#endif
+static_assert(TOP_WAVES_CFG == 4 || TOP_WAVES_CFG == 8, "TOP_WAVES_CFG must be 4 or 8");
+constexpr int TOP_WAVES = TOP_WAVES_CFG / PW_PER_WAVE;
+constexpr int TOP_SLOTS = TOP_WAVES * PW_PER_WAVE;
 // coin_mode (the launch that reaches the root, one workgroup): after the root, wave 0 runs the
 // transcript step that follows the tree -- 1: coin[0] = merge(coin[0], root) (the trace and
 // constraint roots), 2: that and coin[1] = merge_with_int(coin[0], 1) (a FRI layer: alpha) --
@@ -771,6 +778,6 @@ const char* poseidon_build_config() {
       PM_ROW_WAVES_CFG) ";PM_IGLP=" ZKL_STR(PM_IGLP_CFG) ";TAIL_PRIO=" ZKL_STR(TAIL_PRIO_CFG) ";PW_MAX_ITEMS=" ZKL_STR(
       PW_MAX_ITEMS_CFG) ";PM_ROW_BIG=" ZKL_STR(PM_ROW_BIG_CFG) ";POSEIDON_SCHED=" ZKL_STR(
       ZKL_POSEIDON_SCHED_NAME) ";PM_PRUNE=" ZKL_STR(PM_PRUNE_CFG) ";PM_MFMA_PROBE=" ZKL_STR(PM_MFMA_PROBE_CFG)
-      ";TOP_LDS=" ZKL_STR(TOP_LDS_CFG);
+      ";TOP_LDS=" ZKL_STR(TOP_LDS_CFG) ";TOP_WAVES=" ZKL_STR(TOP_WAVES_CFG);
 }
 }  // namespace zkl
