@@ -1,9 +1,9 @@
 // gfx950 Poseidon kernels of the zk-lisp segment prover: hot loop A --
 // partitioned row hashing of the trace and composition LDEs, Merkle levels, FRI layer leaves,
 // transcript draws and grinding -- in the lane-group (latency) and matrix-core (throughput)
-// forms.  A translation unit of its own so it can be compiled with the scheduling strategy
-// that suits its long VALU blocks (Makefile: -amdgpu-sched-strategy=max-ilp) while the NTT,
-// constraint evaluator and DEEP (kernels.hip) keep the default one.
+// forms.  A translation unit of its own so scheduler flags can differ from those of the NTT,
+// constraint evaluator and DEEP (kernels.hip); the default scheduler measured best for both
+// (Makefile: POSEIDON_SCHED).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
