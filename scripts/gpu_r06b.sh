@@ -1,7 +1,8 @@
 #!/bin/bash
 # round 6, second pass: (1) tools/latbench with two independent cube chains per lane (is the
 # 48-lane cube issue-bound or dependency-bound?); (2) the matrix-pipe cost of the unreduced-cube
-# form: row hash with 6 extra zero-B k-steps per tile (PM_MFMA_PROBE_CFG=6, 78 MFMAs per round,
+# form: row hash with 6 extra zero-B k-steps per tile (PM_MFMA_PROBE_CFG=6 with
+# profiles/r06/mfma_probe/probe_variant.patch applied, 78 MFMAs per round,
 # digests unchanged) against the shipped build, hashbench + SQ counters; (3) the caller-Vec
 # penalty broken down by phase (bench host_trace.per_proof_allocation, ZKL_UP_DEBUG upload lines)
 set -u

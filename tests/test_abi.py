@@ -46,7 +46,7 @@ def test_build_carries_only_default_tuning_values():
     assert cfg == {"PM_WAVES": "8", "PM_WIDE": "0", "PM_ROW_WAVES": "8", "PM_IGLP": "0", "TAIL_PRIO": "0",
                    "PW_MAX_ITEMS": "2048", "PM_ROW_BIG": "0", "POSEIDON_SCHED": "default", "NTT_ELEMS": "1024",
                    "NTT_THREADS": "256", "CE_WAVES": "3", "CE_POSE_WAVES": "3", "DEEP_PTS": "2",
-                   "DEEP_COLS": "4", "PM_PRUNE": "3", "PM_MFMA_PROBE": "0", "TOP_LDS": "1", "TOP_WAVES": "4", "CE_GROUPS": "31",
+                   "DEEP_COLS": "4", "PM_PRUNE": "3", "TOP_LDS": "1", "TOP_WAVES": "4", "CE_GROUPS": "31",
                    "CE_DOT": "0", "CE_BRANCHFREE": "0"}
 
 

@@ -777,7 +777,7 @@ const char* poseidon_build_config() {
   return "PM_WAVES=" ZKL_STR(PM_WAVES_CFG) ";PM_WIDE=" ZKL_STR(PM_WIDE_CFG) ";PM_ROW_WAVES=" ZKL_STR(
       PM_ROW_WAVES_CFG) ";PM_IGLP=" ZKL_STR(PM_IGLP_CFG) ";TAIL_PRIO=" ZKL_STR(TAIL_PRIO_CFG) ";PW_MAX_ITEMS=" ZKL_STR(
       PW_MAX_ITEMS_CFG) ";PM_ROW_BIG=" ZKL_STR(PM_ROW_BIG_CFG) ";POSEIDON_SCHED=" ZKL_STR(
-      ZKL_POSEIDON_SCHED_NAME) ";PM_PRUNE=" ZKL_STR(PM_PRUNE_CFG) ";PM_MFMA_PROBE=" ZKL_STR(PM_MFMA_PROBE_CFG)
+      ZKL_POSEIDON_SCHED_NAME) ";PM_PRUNE=" ZKL_STR(PM_PRUNE_CFG)
       ";TOP_LDS=" ZKL_STR(TOP_LDS_CFG) ";TOP_WAVES=" ZKL_STR(TOP_WAVES_CFG);
 }
 }  // namespace zkl
